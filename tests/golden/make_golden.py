@@ -1,0 +1,263 @@
+"""Generate the golden vectors that pin the oracle — run in the BUILD container only.
+
+It imports the reference model (/root/reference/vilbert_k3m/vilbert_k3m.py) and its preprocessing
+(/root/reference/vilbert_k3m/datasets/concept_cap_dataset_struc.py) with stub modules for the
+imports that are not on the pretraining path and not installed here (boto3, tensorboardX,
+torch._six, tensorpack, lmdb, msgpack_numpy) and a character-level stand-in tokenizer (no
+BERT vocab file exists offline).  Only the recorded inputs/outputs are committed
+(``golden_*.npz``); the reference never leaves this container.
+
+Per case:
+* inputs: rows of data/raw_multidata_of_product_preatrain.small_train preprocessed by the
+  reference's BertPreprocessBatch (mask_word / mask_word_pv / index_pv / mask_region) + the
+  global-region collation of ConceptCapLoaderTrain_struc.__iter__ (dataset:381-397) over seeded
+  synthetic region features (no images are bundled);
+* weights: k3m_amd.weights.param_values(cfg, seed) loaded by name;
+* randomness made explicit: F.gumbel_softmax noise regenerated from ``noise_seed`` (numpy), and
+  the LPM ``random.sample`` draws recorded into ent_neg / val_neg tables;
+* model.eval() (dropout off), forward + backward of the driver's summed loss
+  (train_concap_struc.py:531-533).
+
+Usage:  python tests/golden/make_golden.py
+"""
+import math
+import os
+import random
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+
+def _stub_imports():
+    for n in ["boto3", "botocore", "botocore.exceptions", "tensorboardX", "torch._six",
+              "tensorpack", "tensorpack.dataflow", "lmdb", "msgpack_numpy", "msgpack"]:
+        sys.modules.setdefault(n, types.ModuleType(n))
+    sys.modules["botocore.exceptions"].ClientError = type("ClientError", (Exception,), {})
+    sys.modules["tensorboardX"].SummaryWriter = object
+    sys.modules["torch._six"].inf = math.inf
+    td = sys.modules["tensorpack.dataflow"]
+    for c in ["LMDBSerializer", "NumpySerializer", "DataFromList", "MapData", "PrefetchDataZMQ",
+              "BatchData", "RNGDataFlow", "LocallyShuffleData"]:
+        setattr(td, c, type(c, (), {}))
+    sys.modules["tensorpack"].dataflow = td
+    sys.modules["msgpack_numpy"].patch = lambda: None
+    sys.path.insert(0, REF)
+
+
+class CharTokenizer(object):
+    """Stand-in for BertTokenizer(bert-base-chinese): one id per character; the KG separators map
+    to the ids the reference hard-codes (':' -> 131, ';' -> 132; dataset:785-840)."""
+    mask_token = "[MASK]"
+
+    def encode(self, text):
+        out = []
+        for ch in text.replace("#", ""):
+            if ch == ":":
+                out.append(131)
+            elif ch == ";":
+                out.append(132)
+            elif ch.isspace():
+                continue
+            else:
+                out.append(200 + (ord(ch) * 7919) % (21128 - 200))
+        return out
+
+    def convert_tokens_to_ids(self, tok):
+        return {"[MASK]": 103, "[CLS]": 101, "[SEP]": 102, "[PAD]": 0}[tok]
+
+    def add_special_tokens_single_sentence(self, ids):
+        return [101] + list(ids) + [102]
+
+    def __len__(self):
+        return 21128
+
+
+def synth_regions(rng, nbox=36, feat=2048, cls=1601):
+    h, w = 600.0, 800.0
+    x1 = rng.uniform(0, w * 0.7, nbox)
+    y1 = rng.uniform(0, h * 0.7, nbox)
+    x2 = np.minimum(w, x1 + rng.uniform(20, w * 0.3, nbox))
+    y2 = np.minimum(h, y1 + rng.uniform(20, h * 0.3, nbox))
+    boxes = np.stack([x1, y1, x2, y2], 1).astype(np.float32)
+    f = np.abs(rng.standard_normal((nbox, feat))).astype(np.float32) * 0.5
+    logits = rng.standard_normal((nbox, cls)).astype(np.float32) * 2
+    p = np.exp(logits - logits.max(1, keepdims=True))
+    p = (p / p.sum(1, keepdims=True)).astype(np.float32)
+    return h, w, nbox, boxes, f, p
+
+
+def build_batch(pre, rows, seed):
+    random.seed(seed)
+    np.random.seed(seed)
+    rng = np.random.default_rng(seed)
+    samples = []
+    for r in rows:
+        item_id, title, _url, pv, cate = r
+        h, w, nb, boxes, f, p = synth_regions(rng)
+        samples.append(pre((item_id, title, pv, cate, h, w, nb, boxes, f, p)))
+    cols = list(zip(*samples))
+    (item_id, input_ids, input_mask, segment_ids, lm_label_ids, is_next, input_ids_pv, input_mask_pv,
+     segment_ids_pv, lm_label_ids_pv, is_next_pv_v, is_next_pv_t, index_p, index_v, image_feat,
+     image_loc, image_target, image_label, image_mask, masked_label) = [np.stack(c) for c in cols]
+    B = input_ids.shape[0]
+    # global region (ConceptCapLoaderTrain_struc.__iter__, dataset:381-397)
+    cnt = np.sum(masked_label == 0, axis=1, keepdims=True)
+    cnt[cnt == 0] = 1
+    g = np.sum(image_feat, axis=1) / cnt
+    image_feat = np.concatenate([g[:, None], image_feat], 1).astype(np.float32)
+    gl = np.repeat(np.array([[0, 0, 1, 1, 1]], np.float32), B, 0)
+    image_loc = np.concatenate([gl[:, None], image_loc], 1).astype(np.float32)
+    image_mask = np.concatenate([np.ones((B, 1), image_mask.dtype), image_mask], 1)
+    return dict(input_ids=input_ids, input_mask=input_mask, segment_ids=segment_ids, lm_label_ids=lm_label_ids,
+                is_next=is_next, input_ids_pv=input_ids_pv, input_mask_pv=input_mask_pv,
+                segment_ids_pv=segment_ids_pv, lm_label_ids_pv=lm_label_ids_pv, is_next_pv_v=is_next_pv_v,
+                is_next_pv_t=is_next_pv_t, image_feat=image_feat, image_loc=image_loc,
+                image_target=image_target.astype(np.float32), image_label=image_label, image_mask=image_mask,
+                index_p=index_p, index_v=index_v)
+
+
+def gumbel_noise(seed, shapes):
+    rng = np.random.default_rng(seed)
+    return {k: (-np.log(rng.standard_exponential(s))).astype(np.float32) for k, s in shapes}
+
+
+# selected gradients stored in full (small) or as a leading slice (large)
+FULL_GRADS = ["struc_w2.weight", "struc_w2.bias", "struc_w1.bias", "struc_w3.bias", "embeddings.LayerNorm.weight",
+              "encoder.layer.0.attention.output.LayerNorm.bias", "encoder.layer.11.output.dense.bias",
+              "encoder.v_layer.5.output.LayerNorm.weight", "encoder.c_layer.0.biOutput.LayerNorm1.weight",
+              "encoder.c_layer_pv_v.3.t_output.LayerNorm.bias", "encoder.c_layer_pv_t.5.biOutput.dense2.bias",
+              "cls.predictions.transform.LayerNorm.weight", "cls.imagePredictions.decoder.bias",
+              "v_embeddings.LayerNorm.bias", "score_self_t.bias", "map_bi_to_individual.bias",
+              "embeddings.token_type_embeddings.weight"]
+SLICE_GRADS = ["encoder.layer.0.attention.self.query.weight", "encoder.layer.6.intermediate.dense.weight",
+               "encoder.v_layer.0.attention.self.value.weight", "encoder.c_layer.2.biattention.key2.weight",
+               "encoder.c_layer_pv_t.1.biattention.query1.weight", "v_embeddings.image_embeddings.weight",
+               "score_cross2_v.weight", "struc_w1.weight", "cls.predictions.transform.dense.weight",
+               "embeddings.word_embeddings.weight", "cls.predictions.bias"]
+
+
+def run_case(name, row_ids, data_seed, weight_seed, noise_seed, neg_seed, mode=1, T=36, P=128, NPV=20,
+             drop_pv_of=()):
+    import vilbert_k3m.vilbert_k3m as K
+    from vilbert_k3m.datasets.concept_cap_dataset_struc import BertPreprocessBatch
+    from k3m_amd.config import pretrain_config
+    from k3m_amd.weights import param_values
+
+    rows = [l.rstrip("\n").split("\t") for l in open(os.path.join(REF, "data/raw_multidata_of_product_preatrain.small_train"),
+                                                        encoding="utf-8")]
+    rows = [rows[i] for i in row_ids]
+    for i in drop_pv_of:          # an item with no property-value triple (exercises the zero-triple quirk)
+        rows[i] = rows[i][:3] + ["no-properties-here"] + rows[i][4:]
+    pre = BertPreprocessBatch(CharTokenizer(), max_seq_len=T, max_seq_len_pv=P, max_num_pv=NPV, max_region_len=36)
+    batch = build_batch(pre, rows, data_seed)
+
+    cfg_path = os.path.join(REPO, "configs/bert_base_6layer_6conect.json")
+    cfg = pretrain_config(cfg_path, if_pre_sampling=mode)
+    rcfg = K.BertConfig.from_json_file(cfg_path)
+    for k in ("v_target_size", "visual_target", "with_coattention", "dynamic_attention", "if_pre_sampling", "num_negative"):
+        setattr(rcfg, k, getattr(cfg, k))
+    torch.manual_seed(0)
+    model = K.BertForMultiModalPreTraining_tri_stru(rcfg)
+    vals = param_values(cfg, weight_seed)
+    sd = {k: torch.from_numpy(v) for k, v in vals.items()}
+    sd["cls.predictions.decoder.weight"] = sd["embeddings.word_embeddings.weight"]
+    model.load_state_dict(sd)
+    model.tie_weights()
+    model.eval()
+
+    B = batch["input_ids"].shape[0]
+    shapes = [("v", (B, 37, 3, 1024)), ("t", (B, T, 3, 768)), ("pv", (B, P, 3, 768))]
+    noise = {k: torch.from_numpy(v) for k, v in gumbel_noise(noise_seed, shapes).items()}
+    order = {}
+
+    def fake_gumbel(logits, tau=1.0, hard=False, eps=1e-10, dim=-1):
+        L = logits.shape[1]
+        key = "v" if logits.shape[-1] == 1024 else ("t" if L == T else "pv")
+        order.setdefault(key, len(order))
+        g = noise[key]
+        y = ((logits + g) / tau).softmax(dim)
+        idx = y.max(dim, keepdim=True)[1]
+        hardv = torch.zeros_like(logits).scatter_(dim, idx, 1.0)
+        return hardv - y.detach() + y
+
+    draws = []
+    real_sample = random.sample
+
+    def rec_sample(pop, k):
+        r = real_sample(pop, k)
+        draws.append(list(r))
+        return r
+
+    K.F.gumbel_softmax = fake_gumbel
+    random.seed(neg_seed)
+    K.random.sample = rec_sample
+    tb = {k: torch.from_numpy(np.asarray(v)) for k, v in batch.items()}
+    try:
+        out = model(tb["input_ids"], tb["image_feat"], tb["image_loc"], tb["segment_ids"], tb["input_mask"],
+                    tb["image_mask"], tb["lm_label_ids"], tb["image_label"], tb["image_target"], tb["is_next"],
+                    input_ids_pv=tb["input_ids_pv"], token_type_ids_pv=tb["segment_ids_pv"],
+                    attention_mask_pv=tb["input_mask_pv"], masked_lm_labels_pv=tb["lm_label_ids_pv"],
+                    next_sentence_label_pv_v=tb["is_next_pv_v"], next_sentence_label_pv_t=tb["is_next_pv_t"],
+                    index_p=tb["index_p"], index_v=tb["index_v"], device=torch.device("cpu"))
+    finally:
+        K.random.sample = real_sample
+    mlm_t, img, _, mlm_pv, _, _, nsp, c_init, c_final, lpm = out
+    loss = mlm_t + img + mlm_pv + lpm
+    loss.backward()
+    mlm_t, img, mlm_pv, lpm, nsp, loss = [x.detach() for x in (mlm_t, img, mlm_pv, lpm, nsp, loss)]
+
+    # rebuild the negative tables in the reference's draw order (:2472-2497)
+    ent = -np.ones((B, NPV, 2), np.int64)
+    val = -np.ones((B, NPV, 2), np.int64)
+    nvalid = [next((j for j in range(NPV) if batch["index_p"][i, j, 0] == 0), NPV) for i in range(B)]
+    it = iter(draws)
+    for i in range(B):
+        for j in range(nvalid[i]):
+            if B > 1:
+                d = next(it)
+                ent[i, j, :len(d)] = d
+            if nvalid[i] > 1:
+                d = next(it)
+                val[i, j, :len(d)] = d
+    assert next(it, None) is None
+
+    res = {"losses": np.array([float(mlm_t), float(img), float(mlm_pv), float(lpm), float(nsp), float(loss)], np.float64),
+           "c_initial": c_init.detach().numpy(), "c_final": c_final.detach().numpy(),
+           "ent_neg": ent, "val_neg": val, "noise_seed": np.array(noise_seed), "weight_seed": np.array(weight_seed),
+           "mode": np.array(mode), "noise_order": np.array([order.get(k, -1) for k in ("v", "t", "pv")])}
+    params = dict(model.named_parameters())
+    gn_names, gn = [], []
+    for n, p in params.items():
+        gn_names.append(n)
+        gn.append(np.nan if p.grad is None else float(p.grad.double().norm()))
+    res["grad_norm_names"] = np.array(gn_names)
+    res["grad_norms"] = np.array(gn, np.float64)
+    for n in FULL_GRADS:
+        g = params[n].grad
+        res["grad_full/" + n] = np.zeros(tuple(params[n].shape), np.float32) if g is None else g.numpy()
+    for n in SLICE_GRADS:
+        g = params[n].grad
+        if g is None:
+            g = torch.zeros(tuple(params[n].shape))
+        res["grad_slice/" + n] = (g[:4] if g.dim() == 2 else g[:256]).numpy()
+    for k, v in batch.items():
+        res["in/" + k] = np.asarray(v)
+    path = os.path.join(HERE, "golden_%s.npz" % name)
+    np.savez_compressed(path, **res)
+    print(name, "losses", res["losses"], "->", path, os.path.getsize(path) // 1024, "KiB")
+
+
+if __name__ == "__main__":
+    _stub_imports()
+    torch.set_num_threads(8)
+    run_case("bs2_hard", [0, 1], data_seed=7, weight_seed=1234, noise_seed=11, neg_seed=42, mode=1)
+    run_case("bs3_zero_triple", [4, 2, 9], data_seed=8, weight_seed=99, noise_seed=12, neg_seed=43, mode=1,
+             drop_pv_of=(0,))
+    run_case("bs2_mean", [3, 5], data_seed=9, weight_seed=7, noise_seed=13, neg_seed=44, mode=0)
