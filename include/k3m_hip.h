@@ -1,0 +1,211 @@
+/* libk3m_hip — C ABI of the MI355X (gfx950) kernels behind the K3M tri-modal pretraining step.
+ *
+ * Boundary contract:
+ *   - plain device pointers, sizes and a hipStream_t; no torch types;
+ *   - the caller (torch's caching allocator) owns every buffer, including saved activations and
+ *     workspaces; the library allocates nothing and keeps no state;
+ *   - every entry point returns 0 on success, K3M_EINVAL on a bad argument, or -hipError_t of the
+ *     launch; no host synchronisation inside (graph-capturable);
+ *   - all work is enqueued on the passed stream.
+ *
+ * Each entry point names the reference code it replaces (file:line in sunzeyeah/K3M).  The
+ * reference has no native operator API: its hot path is nn.Module code in
+ * vilbert_k3m/vilbert_k3m.py whose ops go to ATen/cuBLAS; these functions are the replacement
+ * kernels for those ops, bound from Python by k3m_amd/_lib.py (ctypes).
+ */
+#ifndef K3M_HIP_H
+#define K3M_HIP_H
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define K3M_OK 0
+#define K3M_EINVAL 1
+
+enum K3mDType { K3M_F32 = 0, K3M_BF16 = 1 };
+
+enum K3mEpilogue {
+  K3M_EPI_NONE = 0,         /* C = alpha*acc + beta*C                                        */
+  K3M_EPI_BIAS = 1,         /* C = alpha*(acc + bias) + beta*C                               */
+  K3M_EPI_BIAS_GELU = 2,    /* aux = acc + bias; C = gelu(aux)            (BertIntermediate)  */
+  K3M_EPI_DGELU = 3,        /* C = acc * gelu'(aux) (+ beta*C)            (its backward)      */
+  K3M_EPI_BIAS_SIGMOID = 4  /* C = sigmoid(acc + bias)                    (fusion gate scores)*/
+};
+
+/* C[m,n] = op(A)[m,k] . op(B)[k,n] with a fused epilogue.
+ *   a_trans = 0: A(i,l) = a[i*lda + l]   (row-major activations, K contiguous)
+ *   a_trans = 1: A(i,l) = a[l*lda + i]   (dY^T for weight gradients)
+ *   b_trans = 1: B(l,j) = b[j*ldb + l]   (torch Linear weight [n,k]: forward x.W^T)
+ *   b_trans = 0: B(l,j) = b[l*ldb + j]   (W for input gradients, X for weight gradients)
+ * Replaces every nn.Linear addmm / mm of the step (vilbert_k3m.py: all Linear layers, tied decoder
+ * :1838) and their autograd backward GEMMs. */
+typedef struct K3mGemm {
+  int m, n, k;
+  int a_trans, b_trans;
+  int epilogue;
+  int dtype;
+  int splitk;            /* >1: K split over splitk workgroup slices (epilogue must be NONE);   */
+  long long lda, ldb, ldc, ldaux;
+  const void* a;
+  const void* b;
+  void* c;
+  const float* bias;
+  void* aux;
+  float* ws;             /* splitk > 1: fp32 workspace of splitk*m*n floats (deterministic    */
+  float alpha, beta;     /* slab reduction, no atomics)                                        */
+} K3mGemm;
+int k3m_gemm(const K3mGemm* g, hipStream_t stream);
+
+/* out[c] (+)= sum_r x[r*ld + c]  — bias gradients (autograd of every Linear bias).
+ * ws: >= 64*cols floats. */
+int k3m_colsum(const void* x, long long ld, int rows, int cols, float* out, int accumulate, float* ws,
+               int dtype, hipStream_t stream);
+
+/* Post-LN residual block tail (BertSelfOutput/BertOutput/BertBiOutput/BertImageEmbeddings,
+ * vilbert_k3m.py:485-489, :528-532, :986-996, :2153-2161, LayerNorm :319-332):
+ *   s = dropout_in(x) + res;  y = dropout_out(gamma * (s-mean)*rstd + beta)
+ * saves xhat = (s-mean)*rstd and rstd for the backward.  res may be NULL. */
+int k3m_ln_fwd(const void* x, const void* res, const float* gamma, const float* beta, void* y, void* xhat,
+               float* rstd, int rows, int cols, float eps, float p_in, float p_out, uint64_t seed,
+               uint64_t off_in, uint64_t off_out, int dtype, hipStream_t stream);
+/* Backward of k3m_ln_fwd.  ds = d(pre-LN sum) is written to dres (or accumulated when
+ * accumulate_res), dx = dropout_in'(ds) is written to dx (may alias dres when p_in == 0).
+ * dgamma/dbeta are ACCUMULATED (fp32 grad buffer).  ws: >= 2*128*cols floats. */
+int k3m_ln_bwd(const void* dy, const void* xhat, const float* rstd, const float* gamma, void* dres, void* dx,
+               float* dgamma, float* dbeta, int rows, int cols, float p_in, float p_out, uint64_t seed,
+               uint64_t off_in, uint64_t off_out, int accumulate_res, float* ws, int dtype, hipStream_t stream);
+
+/* BertEmbeddings (vilbert_k3m.py:361-382): word + position + token-type -> LN -> dropout.
+ * The row is written to y0 and, when non-NULL, to y1 and y2 (the same embedding output feeds two
+ * encoder passes, vilbert_k3m.py:1703-1743).  ids/tt: int64 [nseq, len]. */
+int k3m_embed_fwd(const int64_t* ids, const int64_t* tt, const float* word, const float* pos, const float* type,
+                  const float* gamma, const float* beta, void* y0, void* y1, void* y2, void* xhat, float* rstd,
+                  int nseq, int len, int hidden, float eps, float p_out, uint64_t seed, uint64_t off,
+                  int dtype, hipStream_t stream);
+/* Gradient of the lookup: dword[id] += ds (skipping id 0: padding_idx, :343-345), dpos, dtype.
+ * ds = d(pre-LN sum) from k3m_ln_bwd. */
+int k3m_embed_bwd(const int64_t* ids, const int64_t* tt, const void* ds, float* dword, float* dpos, float* dtype_,
+                  int nseq, int len, int hidden, int dtype, hipStream_t stream);
+
+/* Multi-head scaled-dot-product attention with additive key mask, softmax and probability
+ * dropout (BertSelfAttention :439-475, BertImageSelfAttention :586-634, BertBiAttention :753-838,
+ * BertBiAttention_two_text :882-965).  Row (s, i) of Q starts at q + (s*lq+i)*ldq; head h is
+ * columns [h*hd, (h+1)*hd).  kmask: additive float [nseq, lk].  probs: [nseq, nh, lq, lk]
+ * (softmax output before dropout), saved for the backward. */
+int k3m_attn_fwd(const void* q, long long ldq, const void* k, long long ldk, const void* v, long long ldv,
+                 const float* kmask, void* ctx, long long ldc, float* probs, int nseq, int lq, int lk, int nh, int hd,
+                 float scale, float p_drop, uint64_t seed, uint64_t off, int dtype, hipStream_t stream);
+int k3m_attn_bwd(const void* dctx, long long ldc, const void* q, long long ldq, const void* k, long long ldk,
+                 const void* v, long long ldv, const float* probs, void* dq, void* dk, void* dv, long long lddq,
+                 long long lddk, long long lddv, int nseq, int lq, int lk, int nh, int hd, float scale, float p_drop,
+                 uint64_t seed, uint64_t off, int dtype, hipStream_t stream);
+
+/* Elementwise: out = g * gelu'(pre) (backward of the MLM/image head transforms :1795-1818). */
+int k3m_dgelu(const void* g, const void* pre, void* out, long long n, int dtype, hipStream_t stream);
+
+/* Row gather / scatter-add for the labelled-row heads. idx: int32 [n]. */
+int k3m_gather_rows(const void* src, long long lds, const int32_t* idx, int n, int cols, void* dst, long long ldd,
+                    int dtype, hipStream_t stream);
+int k3m_scatter_add_rows(const void* src, long long lds, const int32_t* idx, int n, int cols, void* dst,
+                         long long ldd, int dtype, hipStream_t stream);
+
+/* Compact labelled positions (order preserving, single workgroup, graph-safe): for r in [0,n) with
+ * labels[r] >= thresh append, at position count[0] + rank,
+ *   idx = (r / inner) * outer + r % inner + base   (row in the sequence buffer),
+ *   out_labels = labels[r], src = r, slot = slot_id,
+ * then row_scale = 1/appended for the appended rows (mean over the task's labelled rows) and
+ * count[0] += appended.  Any of out_labels / src / row_scale / slot may be NULL. */
+int k3m_compact_labels_ex(const int64_t* labels, int n, int64_t thresh, int inner, int outer, int base, int slot_id,
+                          int32_t* idx, int64_t* out_labels, int32_t* src, float* row_scale, int32_t* slot,
+                          int32_t* count, hipStream_t stream);
+
+/* Masked-LM cross-entropy (CrossEntropyLoss(ignore_index=-1), :2255, :2817-2826) over gathered
+ * rows: loss_rows[r] = lse - logit[label]; logits are overwritten by row_scale[r]*(softmax-onehot). */
+int k3m_ce_fwd_bwd(float* logits, long long ld, const int64_t* labels, const float* row_scale, int rows, int vocab,
+                   float* loss_rows, hipStream_t stream);
+/* Region KL (KLDivLoss(log_softmax(pred), target), :2753-2760) over gathered rows: loss_rows[r] =
+ * sum_c xlogy(t,t) - t*logsoftmax(pred); pred overwritten by scale*(softmax*sum(t) - t). */
+int k3m_kl_fwd_bwd(float* logits, long long ld, const float* target, long long ldt, const int32_t* trow,
+                   const float* row_scale, int rows, int ncls, float* loss_rows, hipStream_t stream);
+/* out[slot[r]] += loss_rows[r] * row_scale[r] for slots 0..3 (single block). */
+int k3m_loss_reduce(const float* loss_rows, const float* row_scale, const int32_t* slot, int rows, float* out,
+                    hipStream_t stream);
+/* NSP head forward (seq_relationship(dropout(t+pv+v)) + CE, :1881-1887, :2828-2832); forward only
+ * (its loss is excluded from the training total, train_concap_struc.py:533). */
+int k3m_nsp_loss(const float* pt, const float* ppv, const float* pv, const float* w, const float* b,
+                 const int64_t* l0, const int64_t* l1, const int64_t* l2, int batch, int hidden, float* out,
+                 hipStream_t stream);
+
+/* Fusion gate, pre_sampling_sequence (vilbert_k3m.py:2331-2374):
+ * relu_cat3: c[r, k*D + ch] = relu(x_k[r, ch])                                               */
+int k3m_relu_cat3(const void* x0, const void* x1, const void* x2, void* c, int rows, int d, int dtype,
+                  hipStream_t stream);
+/* gate forward: a = sigmoid scores [rows, 3D]; noise [rows, 3, D] or NULL (then gumbel noise is
+ * drawn from (seed, off)); ys = softmax(a + g) over the 3 streams; idx = argmax; out = c[idx]. */
+int k3m_gate_fwd(const float* a, const void* c, const float* noise, float* ys, uint8_t* idx, void* out, int rows,
+                 int d, uint64_t seed, uint64_t off, int dtype, hipStream_t stream);
+/* gate backward (straight-through): dc = onehot*dout; dpre = sigmoid'(a)*softmax'(ys)(dout*c). */
+int k3m_gate_bwd(const void* dout, const float* a, const void* c, const float* ys, const uint8_t* idx, void* dc,
+                 void* dpre, int rows, int d, int dtype, hipStream_t stream);
+/* dx_k (+)= dc[:, kD:(k+1)D] * (c > 0), k = 0..2 (any dx_k may be NULL). */
+int k3m_relu_split3_bwd(const void* dc, const void* c, void* dx0, void* dx1, void* dx2, int rows, int d,
+                        int accumulate, int dtype, hipStream_t stream);
+/* if_pre_sampling == 0: out = (x0+x1+x2)/3 ; backward: dx_k (+)= dout/3 */
+int k3m_mean3(const void* x0, const void* x1, const void* x2, void* out, long long n, int dtype, hipStream_t stream);
+int k3m_mean3_bwd(const void* dout, void* dx0, void* dx1, void* dx2, long long n, int accumulate, int dtype,
+                  hipStream_t stream);
+/* out[s, :] (+)= scale * mean(x[s, start:len, :])  (pooled outputs :2405-2409) and backward. */
+int k3m_seq_mean(const void* x, int nseq, int len, int start, int d, float scale, float* out, int accumulate,
+                 int dtype, hipStream_t stream);
+int k3m_seq_mean_bwd(const float* dout, int nseq, int len, int start, int d, float scale, void* dx, int dtype,
+                     hipStream_t stream);
+
+/* Structure aggregator + LPM (structure_aggregator, vilbert_k3m.py:2413-2505), vectorised over a
+ * padded [B, NPV] triple layout.  X[(i*npv+j), :] = [c_init_i ; p_ij ; v_ij] with p/v the mean of
+ * the two endpoint rows of index_p/index_v; nvalid[i] = first j with index_p[i,j,0]==0. */
+int k3m_sa_gather(const void* seq, const int64_t* index_p, const int64_t* index_v, const float* c_init, float* X,
+                  int32_t* nvalid, int32_t* src, int batch, int len, int npv, int hidden, int dtype,
+                  hipStream_t stream);
+/* per item: beta_j = w2.leaky_relu(T_j) + b2, att = softmax_j, agg = sum_j att_j T_j
+ * (T rows of item src[i]; src[i] = -1 -> agg = c_init[0]). */
+int k3m_sa_attn_fwd(const float* T, const int32_t* nvalid, const int32_t* src, const float* w2, const float* b2,
+                    const float* c_init, float* att, float* agg, int batch, int npv, int hidden, hipStream_t stream);
+int k3m_sa_attn_bwd(const float* dagg, const float* T, const float* att, const int32_t* nvalid,
+                    const int32_t* src, const float* w2, float* dT, float* dw2, float* db2, float* dc_init, int batch,
+                    int npv, int hidden, hipStream_t stream);
+/* LPM margin-ranking loss; ent_neg / val_neg [B, NPV, 2] int64 (-1 = none).  loss[0] = mean hinge.
+ * Backward ACCUMULATES into dc_final [B,H] and the p/v thirds of dX. */
+int k3m_lpm_fwd(const float* c_final, const float* X, const int32_t* nvalid, const int64_t* ent_neg,
+                const int64_t* val_neg, int batch, int npv, int hidden, float margin, float* loss, float* ws,
+                hipStream_t stream);
+int k3m_lpm_bwd(const float* c_final, const float* X, const int32_t* nvalid, const int64_t* ent_neg,
+                const int64_t* val_neg, int batch, int npv, int hidden, float margin, const float* ws,
+                float* dc_final, float* dX, hipStream_t stream);
+/* Device-side draw of the LPM negatives with the reference's semantics (random.sample without
+ * replacement of min(#candidates, 2) entity indices k != i and value indices j' != j). */
+int k3m_lpm_sample(const int32_t* nvalid, int batch, int npv, int n_ent, int n_val, uint64_t seed, uint64_t off,
+                   int64_t* ent_neg, int64_t* val_neg, hipStream_t stream);
+/* scatter the p / v gradients of dX back to the sequence rows and dX's c_init third into dc_init. */
+int k3m_sa_gather_bwd(const float* dX, const int64_t* index_p, const int64_t* index_v, const int32_t* nvalid,
+                      void* dseq, float* dc_init, int batch, int len, int npv, int hidden, int dtype,
+                      hipStream_t stream);
+
+/* pytorch_transformers 1.1.0 AdamW (train_concap_struc.py:436-441) over a contiguous segment of
+ * the flat parameter buffer: m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
+ * p -= lr*sqrt(1-b2^t)/(1-b1^t) * m/(sqrt(v)+eps); p -= lr*wd*p.  Optionally writes a bf16 copy
+ * of the updated parameters (p_bf16 may be NULL).  grad_scale multiplies g (1/world_size). */
+int k3m_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, long long n, float lr, float beta1,
+              float beta2, float eps, float wd, int step, float grad_scale, hipStream_t stream);
+
+/* Cast helpers for the mixed-precision path. */
+int k3m_cast_f32_bf16(const float* x, uint16_t* y, long long n, hipStream_t stream);
+int k3m_add_inplace(void* y, const void* x, long long n, float alpha, int dtype, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

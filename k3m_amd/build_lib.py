@@ -1,0 +1,52 @@
+"""Build libk3m_hip.so (gfx950) in-tree with hipcc — no torch headers, C ABI only."""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "libk3m_hip.so")
+SOURCES = ["gemm.hip", "gemm_bf16.hip", "norm.hip", "attention.hip", "loss.hip", "fusion.hip", "struct.hip", "adamw.hip"]
+FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-mcode-object-version=5", "-Wno-unused-result"]
+
+
+def hipcc():
+    for p in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc"):
+        if p and os.path.exists(p):
+            return p
+    return "hipcc"
+
+
+def build(force=False, jobs=8, verbose=False):
+    srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    objdir = os.path.join(HERE, "build")
+    os.makedirs(objdir, exist_ok=True)
+    deps = [os.path.join(CSRC, "common.h"), os.path.join(os.path.dirname(HERE), "include", "k3m_hip.h")]
+    dep_m = max(os.path.getmtime(d) for d in deps)
+
+    def one(src):
+        s = os.path.join(CSRC, src)
+        o = os.path.join(objdir, src + ".o")
+        if not force and os.path.exists(o) and os.path.getmtime(o) >= max(os.path.getmtime(s), dep_m):
+            return o
+        cmd = [hipcc()] + FLAGS + ["-c", s, "-o", o]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("hipcc failed for %s:\n%s" % (src, r.stderr[-4000:]))
+        if verbose:
+            print("built", src, file=sys.stderr)
+        return o
+
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(one, srcs))
+    if force or not os.path.exists(OUT) or os.path.getmtime(OUT) < max(os.path.getmtime(o) for o in objs):
+        cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("link failed:\n%s" % r.stderr[-4000:])
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,61 @@
+// AdamW with pytorch_transformers 1.1.0 semantics (the optimizer of train_concap_struc.py:436-441)
+// over a contiguous segment of the flat parameter buffer: one launch updates every tensor of a
+// weight-decay group.  HBM-bound: 16 B read + 12 B written per fp32 parameter (+2 B for the
+// optional bf16 shadow used by the mixed-precision GEMMs).
+#include <cmath>
+#include "common.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    uint16_t* __restrict__ pb, long long n4, float b1, float omb1,
+                                                    float b2, float omb2, float eps, float step_size, float decay,
+                                                    float gscale) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    floatx4 pp = reinterpret_cast<floatx4*>(p)[i];
+    floatx4 gg = reinterpret_cast<const floatx4*>(g)[i];
+    floatx4 mm = reinterpret_cast<floatx4*>(m)[i];
+    floatx4 vv = reinterpret_cast<floatx4*>(v)[i];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float gr = gg[q] * gscale;
+      // exp_avg.mul_(beta1).add_(1 - beta1, grad)
+      mm[q] = mm[q] * b1 + omb1 * gr;
+      // exp_avg_sq.mul_(beta2).addcmul_(1 - beta2, grad, grad)
+      vv[q] = vv[q] * b2 + omb2 * gr * gr;
+      // denom = exp_avg_sq.sqrt().add_(eps); p.addcdiv_(-step_size, exp_avg, denom)
+      const float denom = sqrtf(vv[q]) + eps;
+      pp[q] = pp[q] + (-step_size) * (mm[q] / denom);
+      // p.add_(-lr * weight_decay, p)
+      if (decay != 0.f) pp[q] = pp[q] + (-decay) * pp[q];
+    }
+    reinterpret_cast<floatx4*>(p)[i] = pp;
+    reinterpret_cast<floatx4*>(m)[i] = mm;
+    reinterpret_cast<floatx4*>(v)[i] = vv;
+    if (pb) {
+      uint2 u;
+      u.x = (uint32_t)from_f<bf16_t>(pp[0]).x | ((uint32_t)from_f<bf16_t>(pp[1]).x << 16);
+      u.y = (uint32_t)from_f<bf16_t>(pp[2]).x | ((uint32_t)from_f<bf16_t>(pp[3]).x << 16);
+      reinterpret_cast<uint2*>(pb)[i] = u;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int k3m_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, long long n, float lr,
+                         float beta1, float beta2, float eps, float wd, int step, float grad_scale, hipStream_t st) {
+  K3M_ARG(p && g && m && v && n >= 0 && n % 4 == 0 && step >= 1);
+  K3M_ARG(((uintptr_t)p & 15) == 0 && ((uintptr_t)g & 15) == 0 && ((uintptr_t)m & 15) == 0 && ((uintptr_t)v & 15) == 0);
+  if (n == 0) return 0;
+  const double bc1 = 1.0 - std::pow((double)beta1, step), bc2 = 1.0 - std::pow((double)beta2, step);
+  const float step_size = (float)((double)lr * std::sqrt(bc2) / bc1);
+  const float decay = wd > 0.f ? (float)((double)lr * (double)wd) : 0.f;
+  const long long n4 = n / 4;
+  const int blocks = (int)std::min<long long>((n4 + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, st, p, g, m, v, p_bf16, n4, beta1, 1.f - beta1, beta2,
+                     1.f - beta2, eps, step_size, decay, grad_scale);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,110 @@
+// Shared device helpers for libk3m_hip (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/k3m_hip.h"
+
+#define K3M_CHECK_LAUNCH()                                   \
+  do {                                                       \
+    hipError_t _e = hipGetLastError();                       \
+    if (_e != hipSuccess) return -(int)_e;                   \
+  } while (0)
+
+#define K3M_ARG(cond)                                        \
+  do {                                                       \
+    if (!(cond)) return K3M_EINVAL;                          \
+  } while (0)
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------- bf16 storage type
+struct bf16_t {
+  uint16_t x;
+};
+
+__device__ __forceinline__ float to_f(float v) { return v; }
+__device__ __forceinline__ float to_f(bf16_t v) { return __uint_as_float(((uint32_t)v.x) << 16); }
+template <typename T> __device__ __forceinline__ T from_f(float v);
+template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float v) {
+  uint32_t u = __float_as_uint(v);
+  bf16_t r;
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) {
+    r.x = (uint16_t)((u >> 16) | 0x40);  // keep NaN a NaN
+  } else {
+    r.x = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);  // round to nearest even
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------- counter-based RNG
+// Stateless: every dropout / gumbel site draws u(seed, offset + element) so the backward pass
+// regenerates the forward mask instead of storing it.
+__device__ __forceinline__ uint32_t k3m_hash(uint64_t seed, uint64_t ctr) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (ctr + 1ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+// keep with probability (1-p): returns scale 1/(1-p) or 0.
+__device__ __forceinline__ float k3m_dropout_scale(uint64_t seed, uint64_t ctr, float p) {
+  if (p <= 0.f) return 1.f;
+  uint32_t h = k3m_hash(seed, ctr);
+  float u = (float)(h >> 8) * (1.0f / 16777216.0f);
+  return u >= p ? 1.f / (1.f - p) : 0.f;
+}
+// uniform in (0, 1]
+__device__ __forceinline__ float k3m_uniform(uint64_t seed, uint64_t ctr) {
+  uint32_t h = k3m_hash(seed, ctr);
+  return ((float)(h >> 8) + 1.0f) * (1.0f / 16777216.0f);
+}
+
+// ---------------------------------------------------------------- reductions (wave64)
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// block-wide sum for blockDim.x == 64*NW; red must hold NW floats; result broadcast to all.
+template <int NW>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) s += red[i];
+  return s;
+}
+template <int NW>
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float s = red[0];
+#pragma unroll
+  for (int i = 1; i < NW; ++i) s = fmaxf(s, red[i]);
+  return s;
+}
+
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float dgelu_f(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.3989422804014327f * expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+static inline int k3m_cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }

@@ -1,0 +1,283 @@
+// MFMA GEMM for gfx950 with fused epilogues.
+//
+// fp32 path: v_mfma_f32_32x32x2_f32 (exact f32 fma chain, 155 TF/s peak), 128x128x32 block tile,
+// 4 waves in 2x2, each wave 64x64 = 2x2 MFMA tiles (64 accumulator VGPRs).  LDS holds both
+// operands k-major ([BK][BM+pad]) so every MFMA operand read is a conflict-free ds_read_b32 over
+// 32 consecutive floats.  Global->LDS staging is register double-buffered: the next K-tile's
+// global loads are issued before the current tile's MFMAs and written to the other LDS buffer
+// after them (one barrier per K-tile).
+//
+// Operand layouts (see include/k3m_hip.h): "K-contiguous" (x.W^T activations and torch Linear
+// weights) and "MN-contiguous" (dY^T and X for weight gradients, W for input gradients) are both
+// loaded with 16-byte vectors along their contiguous axis; the K-contiguous case is transposed
+// while being written to LDS.  Split-K writes fp32 slabs reduced deterministically by a second
+// kernel (weight gradients reduce over ~20k rows and have few output tiles).
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
+constexpr int LDSA = BM + 4, LDSB = BN + 4;
+
+// Load one operand tile (BK x TILE) for k0.. into 4 float4 registers per thread.
+// KC = operand is K-contiguous in memory (element (mn, k) at p[mn*ld + k]); else MN-contiguous
+// (element (mn, k) at p[k*ld + mn]).
+template <bool KC, bool VEC, int TILE>
+__device__ __forceinline__ void load_tile(const float* __restrict__ p, long long ld, int mn0, int k0, int MN, int K,
+                                          floatx4 (&r)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    if constexpr (KC) {
+      const int mn = t & (TILE - 1);
+      const int kq = (t >> 7) + 2 * it;  // 0..7
+      const int gm = mn0 + mn, gk = k0 + kq * 4;
+      if constexpr (VEC) {
+        if (gm < MN && gk < K) {
+          r[it] = *reinterpret_cast<const floatx4*>(p + (long long)gm * ld + gk);
+        } else {
+          r[it] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) r[it][q] = (gm < MN && gk + q < K) ? p[(long long)gm * ld + gk + q] : 0.f;
+      }
+    } else {
+      const int kr = (t >> 5) + 8 * it;  // 0..31
+      const int c4 = (t & 31) * 4;
+      const int gk = k0 + kr, gm = mn0 + c4;
+      if constexpr (VEC) {
+        if (gk < K && gm < MN) {
+          r[it] = *reinterpret_cast<const floatx4*>(p + (long long)gk * ld + gm);
+        } else {
+          r[it] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) r[it][q] = (gk < K && gm + q < MN) ? p[(long long)gk * ld + gm + q] : 0.f;
+      }
+    }
+  }
+}
+
+template <bool KC, int TILE, int LDST>
+__device__ __forceinline__ void store_tile(float* __restrict__ s, const floatx4 (&r)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    if constexpr (KC) {
+      const int mn = t & (TILE - 1);
+      const int kq = (t >> 7) + 2 * it;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s[(kq * 4 + q) * LDST + mn] = r[it][q];
+    } else {
+      const int kr = (t >> 5) + 8 * it;
+      const int c4 = (t & 31) * 4;
+      *reinterpret_cast<floatx4*>(s + kr * LDST + c4) = r[it];
+    }
+  }
+}
+
+__device__ __forceinline__ int xcd_remap(int id, int nblk) {
+  // bijective: blocks dispatched round-robin over 8 XCDs -> contiguous id ranges per XCD
+  const int xcd = id & 7, q = nblk >> 3, rr = nblk & 7;
+  const int base = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
+  return base + (id >> 3);
+}
+
+template <bool AK, bool BK_, bool AV, bool BV, int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(K3mGemm g) {
+  __shared__ float As[2][BK * LDSA];
+  __shared__ float Bs[2][BK * LDSB];
+  const int M = g.m, N = g.n, K = g.k;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  const int nblk = tm * tn;
+  int id = xcd_remap(blockIdx.x, nblk);
+  // grouped ordering: GROUP rows of tiles walk N together (L2 reuse of the A panel)
+  constexpr int GROUP = 8;
+  const int group_sz = GROUP * tn;
+  const int gidx = id / group_sz;
+  const int first_m = gidx * GROUP;
+  const int gm_sz = min(tm - first_m, GROUP);
+  const int bm = first_m + (id % group_sz) % gm_sz;
+  const int bn = (id % group_sz) / gm_sz;
+  const int m0 = bm * BM, n0 = bn * BN;
+
+  // split-K range
+  int kbeg = 0, kend = K;
+  if (g.splitk > 1) {
+    const int per = ((K + g.splitk - 1) / g.splitk + BK - 1) / BK * BK;
+    kbeg = blockIdx.y * per;
+    kend = min(K, kbeg + per);
+  }
+  const float* A = static_cast<const float*>(g.a);
+  const float* B = static_cast<const float*>(g.b);
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  floatx4 ra[4], rb[4];
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  if (nk > 0) {
+    load_tile<AK, AV, BM>(A, g.lda, m0, kbeg, M, kend, ra);
+    load_tile<BK_, BV, BN>(B, g.ldb, n0, kbeg, N, kend, rb);
+    store_tile<AK, BM, LDSA>(As[0], ra);
+    store_tile<BK_, BN, LDSB>(Bs[0], rb);
+  }
+  __syncthreads();
+  const int kl = lane >> 5, cl = lane & 31;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      const int k0 = kbeg + (kt + 1) * BK;
+      load_tile<AK, AV, BM>(A, g.lda, m0, k0, M, kend, ra);
+      load_tile<BK_, BV, BN>(B, g.ldb, n0, k0, N, kend, rb);
+    }
+    const float* as = As[cur];
+    const float* bs = Bs[cur];
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2) {
+      const float a0 = as[(kk + kl) * LDSA + wm + cl];
+      const float a1 = as[(kk + kl) * LDSA + wm + 32 + cl];
+      const float b0 = bs[(kk + kl) * LDSB + wn + cl];
+      const float b1 = bs[(kk + kl) * LDSB + wn + 32 + cl];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (more) {
+      store_tile<AK, BM, LDSA>(As[cur ^ 1], ra);
+      store_tile<BK_, BN, LDSB>(Bs[cur ^ 1], rb);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: acc[i][j][r] -> row (r&3) + 8*(r>>2) + 4*(lane>>5), col lane&31
+  float* C = static_cast<float*>(g.c);
+  long long ldc = g.ldc;
+  if (g.splitk > 1) {
+    C = g.ws + (long long)blockIdx.y * M * N;
+    ldc = N;
+  }
+  const float* bias = g.bias;
+  float* aux = static_cast<float*>(g.aux);
+  const float alpha = g.alpha, beta = g.beta;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn + j * 32 + cl;
+      if (col >= N) continue;
+      float bcol = 0.f;
+      if constexpr (EPI == K3M_EPI_BIAS || EPI == K3M_EPI_BIAS_GELU || EPI == K3M_EPI_BIAS_SIGMOID) bcol = bias[col];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
+        if (row >= M) continue;
+        const float v = acc[i][j][r];
+        float* cp = C + (long long)row * ldc + col;
+        if constexpr (EPI == K3M_EPI_NONE) {
+          float o = alpha * v;
+          if (g.splitk <= 1 && beta != 0.f) o += beta * *cp;
+          *cp = o;
+        } else if constexpr (EPI == K3M_EPI_BIAS) {
+          float o = alpha * (v + bcol);
+          if (beta != 0.f) o += beta * *cp;
+          *cp = o;
+        } else if constexpr (EPI == K3M_EPI_BIAS_GELU) {
+          const float pre = v + bcol;
+          aux[(long long)row * g.ldaux + col] = pre;
+          *cp = gelu_f(pre);
+        } else if constexpr (EPI == K3M_EPI_DGELU) {
+          float o = alpha * v * dgelu_f(aux[(long long)row * g.ldaux + col]);
+          if (beta != 0.f) o += beta * *cp;
+          *cp = o;
+        } else {  // BIAS_SIGMOID
+          *cp = sigmoid_f(v + bcol);
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
+                                                            float* __restrict__ C, long long ldc, float alpha,
+                                                            float beta) {
+  const long long total = (long long)M * N;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += ws[(long long)k * total + e];
+    const int row = (int)(e / N), col = (int)(e % N);
+    float* cp = C + (long long)row * ldc + col;
+    float o = alpha * s;
+    if (beta != 0.f) o += beta * *cp;
+    *cp = o;
+  }
+}
+
+template <bool AK, bool BK_, bool AV, bool BV>
+int launch_epi(const K3mGemm& g, hipStream_t st) {
+  const int tm = (g.m + BM - 1) / BM, tn = (g.n + BN - 1) / BN;
+  dim3 grid(tm * tn, g.splitk > 1 ? g.splitk : 1);
+  switch (g.epilogue) {
+    case K3M_EPI_NONE: hipLaunchKernelGGL((gemm_f32_kernel<AK, BK_, AV, BV, K3M_EPI_NONE>), grid, dim3(NT), 0, st, g); break;
+    case K3M_EPI_BIAS: hipLaunchKernelGGL((gemm_f32_kernel<AK, BK_, AV, BV, K3M_EPI_BIAS>), grid, dim3(NT), 0, st, g); break;
+    case K3M_EPI_BIAS_GELU: hipLaunchKernelGGL((gemm_f32_kernel<AK, BK_, AV, BV, K3M_EPI_BIAS_GELU>), grid, dim3(NT), 0, st, g); break;
+    case K3M_EPI_DGELU: hipLaunchKernelGGL((gemm_f32_kernel<AK, BK_, AV, BV, K3M_EPI_DGELU>), grid, dim3(NT), 0, st, g); break;
+    case K3M_EPI_BIAS_SIGMOID: hipLaunchKernelGGL((gemm_f32_kernel<AK, BK_, AV, BV, K3M_EPI_BIAS_SIGMOID>), grid, dim3(NT), 0, st, g); break;
+    default: return K3M_EINVAL;
+  }
+  return 0;
+}
+
+template <bool AK, bool BK_>
+int launch_vec(const K3mGemm& g, bool av, bool bv, hipStream_t st) {
+  if (av && bv) return launch_epi<AK, BK_, true, true>(g, st);
+  if (av) return launch_epi<AK, BK_, true, false>(g, st);
+  if (bv) return launch_epi<AK, BK_, false, true>(g, st);
+  return launch_epi<AK, BK_, false, false>(g, st);
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
+  if (!gp) return K3M_EINVAL;
+  const K3mGemm& g = *gp;
+  K3M_ARG(g.m >= 0 && g.n >= 0 && g.k >= 0);
+  if (g.m == 0 || g.n == 0) return 0;
+  K3M_ARG(g.dtype == K3M_F32);
+  K3M_ARG(g.a && g.b && g.c);
+  K3M_ARG(g.splitk <= 1 || (g.epilogue == K3M_EPI_NONE && g.ws));
+  K3M_ARG(g.epilogue == K3M_EPI_NONE || g.epilogue == K3M_EPI_DGELU || g.bias);
+  K3M_ARG((g.epilogue != K3M_EPI_BIAS_GELU && g.epilogue != K3M_EPI_DGELU) || g.aux);
+  // A: K-contiguous iff a_trans == 0; B: K-contiguous iff b_trans == 1
+  const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
+  const bool av = aligned16(g.a) && (g.lda % 4 == 0) && ((ak ? g.k : g.m) % 4 == 0);
+  const bool bv = aligned16(g.b) && (g.ldb % 4 == 0) && ((bk ? g.k : g.n) % 4 == 0);
+  int rc;
+  if (ak && bk) rc = launch_vec<true, true>(g, av, bv, st);
+  else if (ak && !bk) rc = launch_vec<true, false>(g, av, bv, st);
+  else if (!ak && bk) rc = launch_vec<false, true>(g, av, bv, st);
+  else rc = launch_vec<false, false>(g, av, bv, st);
+  if (rc) return rc;
+  K3M_CHECK_LAUNCH();
+  if (g.splitk > 1) {
+    const long long total = (long long)g.m * g.n;
+    const int blocks = (int)std::min<long long>((total + 255) / 256, 2048);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, g.ws, g.splitk, g.m, g.n,
+                       static_cast<float*>(g.c), g.ldc, g.alpha, g.beta);
+    K3M_CHECK_LAUNCH();
+  }
+  return 0;
+}

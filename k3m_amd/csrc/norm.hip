@@ -1,0 +1,423 @@
+// Row kernels: LayerNorm (+dropout +residual) forward/backward, embeddings, column sums,
+// elementwise helpers.  HBM-bound; one wave per row, 16-byte vectors along the row.
+#include "common.h"
+
+namespace {
+
+constexpr int MAXV = 4;  // float4 chunks per lane: cols <= 64*4*4 = 1024
+
+template <typename T>
+__device__ __forceinline__ floatx4 ld4(const T* p);
+template <>
+__device__ __forceinline__ floatx4 ld4<float>(const float* p) {
+  return *reinterpret_cast<const floatx4*>(p);
+}
+template <>
+__device__ __forceinline__ floatx4 ld4<bf16_t>(const bf16_t* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return floatx4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                 __uint_as_float(u.y & 0xffff0000u)};
+}
+template <typename T>
+__device__ __forceinline__ void st4(T* p, floatx4 v);
+template <>
+__device__ __forceinline__ void st4<float>(float* p, floatx4 v) {
+  *reinterpret_cast<floatx4*>(p) = v;
+}
+template <>
+__device__ __forceinline__ void st4<bf16_t>(bf16_t* p, floatx4 v) {
+  uint2 u;
+  u.x = (uint32_t)from_f<bf16_t>(v[0]).x | ((uint32_t)from_f<bf16_t>(v[1]).x << 16);
+  u.y = (uint32_t)from_f<bf16_t>(v[2]).x | ((uint32_t)from_f<bf16_t>(v[3]).x << 16);
+  *reinterpret_cast<uint2*>(p) = u;
+}
+
+// ------------------------------------------------------------------ LayerNorm forward
+template <typename T>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     T* __restrict__ y, T* __restrict__ xhat, float* __restrict__ rstd,
+                                                     int rows, int cols, float eps, float p_in, float p_out,
+                                                     uint64_t seed, uint64_t off_in, uint64_t off_out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int nv = cols >> 8;  // float4 chunks per lane
+  const long long base = (long long)row * cols;
+  floatx4 v[MAXV];
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    if (j < nv) {
+      const int c = (lane + 64 * j) * 4;
+      floatx4 a = ld4<T>(x + base + c);
+      if (p_in > 0.f) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] *= k3m_dropout_scale(seed, off_in + base + c + q, p_in);
+      }
+      if (res) a += ld4<T>(res + base + c);
+      v[j] = a;
+      sum += a[0] + a[1] + a[2] + a[3];
+    }
+  }
+  const float mean = wave_sum(sum) / cols;
+  float sq = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j)
+    if (j < nv) {
+      v[j] -= mean;
+      sq += v[j][0] * v[j][0] + v[j][1] * v[j][1] + v[j][2] * v[j][2] + v[j][3] * v[j][3];
+    }
+  const float var = wave_sum(sq) / cols;
+  const float rs = 1.0f / sqrtf(var + eps);
+  if (lane == 0 && rstd) rstd[row] = rs;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j)
+    if (j < nv) {
+      const int c = (lane + 64 * j) * 4;
+      const floatx4 xh = v[j] * rs;
+      if (xhat) st4<T>(xhat + base + c, xh);
+      const floatx4 g = *reinterpret_cast<const floatx4*>(gamma + c);
+      const floatx4 b = *reinterpret_cast<const floatx4*>(beta + c);
+      floatx4 o = g * xh + b;
+      if (p_out > 0.f) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] *= k3m_dropout_scale(seed, off_out + base + c + q, p_out);
+      }
+      st4<T>(y + base + c, o);
+    }
+}
+
+// ------------------------------------------------------------------ LayerNorm backward
+constexpr int LN_BWD_BLOCKS = 128;
+
+template <typename T>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ xhat,
+                                                     const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                                     T* __restrict__ dres, T* __restrict__ dx, float* __restrict__ ws,
+                                                     int rows, int cols, float p_in, float p_out, uint64_t seed,
+                                                     uint64_t off_in, uint64_t off_out, int acc_res) {
+  __shared__ float red[2][4][1024];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nv = cols >> 8;
+  floatx4 pg[MAXV], pb[MAXV];
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    pg[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    pb[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int row = blockIdx.x * 4 + w; row < rows; row += gridDim.x * 4) {
+    const long long base = (long long)row * cols;
+    floatx4 dyl[MAXV], xh[MAXV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j)
+      if (j < nv) {
+        const int c = (lane + 64 * j) * 4;
+        floatx4 d = ld4<T>(dy + base + c);
+        if (p_out > 0.f) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) d[q] *= k3m_dropout_scale(seed, off_out + base + c + q, p_out);
+        }
+        const floatx4 xv = ld4<T>(xhat + base + c);
+        dyl[j] = d;
+        xh[j] = xv;
+        pg[j] += d * xv;
+        pb[j] += d;
+        const floatx4 g = *reinterpret_cast<const floatx4*>(gamma + c);
+        const floatx4 dxh = d * g;
+        s1 += dxh[0] + dxh[1] + dxh[2] + dxh[3];
+        s2 += dxh[0] * xv[0] + dxh[1] * xv[1] + dxh[2] * xv[2] + dxh[3] * xv[3];
+      }
+    const float m1 = wave_sum(s1) / cols, m2 = wave_sum(s2) / cols;
+    const float rs = rstd[row];
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j)
+      if (j < nv) {
+        const int c = (lane + 64 * j) * 4;
+        const floatx4 g = *reinterpret_cast<const floatx4*>(gamma + c);
+        floatx4 ds = (dyl[j] * g - m1 - xh[j] * m2) * rs;
+        floatx4 dr = ds;
+        if (acc_res) dr += ld4<T>(dres + base + c);
+        st4<T>(dres + base + c, dr);
+        if (dx != dres) {
+          if (p_in > 0.f) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ds[q] *= k3m_dropout_scale(seed, off_in + base + c + q, p_in);
+          }
+          st4<T>(dx + base + c, ds);
+        }
+      }
+  }
+  // combine the 4 waves' column partials, write this block's slab
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j)
+    if (j < nv) {
+      const int c = (lane + 64 * j) * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        red[0][w][c + q] = pg[j][q];
+        red[1][w][c + q] = pb[j][q];
+      }
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    ws[(long long)blockIdx.x * cols + c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+    ws[(long long)(gridDim.x + blockIdx.x) * cols + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+  }
+}
+
+__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ ws, int nslab, int cols,
+                                                       float* __restrict__ out, int accumulate) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int k = 0; k < nslab; ++k) s += ws[(long long)k * cols + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+// ------------------------------------------------------------------ embeddings
+template <typename T>
+__global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ ids, const int64_t* __restrict__ tt,
+                                                        const float* __restrict__ word, const float* __restrict__ pos,
+                                                        const float* __restrict__ typ, const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, T* y0, T* y1, T* y2, T* xhat,
+                                                        float* rstd, int rows, int len, int cols, float eps,
+                                                        float p_out, uint64_t seed, uint64_t off) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int nv = cols >> 8;
+  const long long id = ids[row], t = tt[row];
+  const int l = row % len;
+  floatx4 v[MAXV];
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j)
+    if (j < nv) {
+      const int c = (lane + 64 * j) * 4;
+      v[j] = *reinterpret_cast<const floatx4*>(word + id * cols + c) +
+             *reinterpret_cast<const floatx4*>(pos + (long long)l * cols + c) +
+             *reinterpret_cast<const floatx4*>(typ + t * cols + c);
+      sum += v[j][0] + v[j][1] + v[j][2] + v[j][3];
+    }
+  const float mean = wave_sum(sum) / cols;
+  float sq = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j)
+    if (j < nv) {
+      v[j] -= mean;
+      sq += v[j][0] * v[j][0] + v[j][1] * v[j][1] + v[j][2] * v[j][2] + v[j][3] * v[j][3];
+    }
+  const float rs = 1.0f / sqrtf(wave_sum(sq) / cols + eps);
+  if (lane == 0) rstd[row] = rs;
+  const long long base = (long long)row * cols;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j)
+    if (j < nv) {
+      const int c = (lane + 64 * j) * 4;
+      const floatx4 xh = v[j] * rs;
+      st4<T>(xhat + base + c, xh);
+      floatx4 o = *reinterpret_cast<const floatx4*>(gamma + c) * xh + *reinterpret_cast<const floatx4*>(beta + c);
+      if (p_out > 0.f) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] *= k3m_dropout_scale(seed, off + base + c + q, p_out);
+      }
+      st4<T>(y0 + base + c, o);
+      if (y1) st4<T>(y1 + base + c, o);
+      if (y2) st4<T>(y2 + base + c, o);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restrict__ ids, const int64_t* __restrict__ tt,
+                                                        const T* __restrict__ ds, float* dword, float* dpos,
+                                                        float* dtyp, int rows, int len, int cols) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const long long id = ids[row], t = tt[row];
+  const int l = row % len;
+  const long long base = (long long)row * cols;
+  for (int c = lane; c < cols; c += 64) {
+    const float g = to_f(ds[base + c]);
+    if (id != 0) atomicAdd(dword + id * cols + c, g);
+    atomicAdd(dpos + (long long)l * cols + c, g);
+    atomicAdd(dtyp + t * cols + c, g);
+  }
+}
+
+// ------------------------------------------------------------------ column sums
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, long long ld, int rows, int cols,
+                                                     float* __restrict__ ws) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  const int chunk = (rows + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * chunk, r1 = min(rows, r0 + chunk);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += to_f(x[(long long)r * ld + c]);
+  ws[(long long)blockIdx.y * cols + c] = s;
+}
+
+// ------------------------------------------------------------------ elementwise
+template <typename T>
+__global__ void dgelu_kernel(const T* g, const T* pre, T* out, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    out[i] = from_f<T>(to_f(g[i]) * dgelu_f(to_f(pre[i])));
+}
+template <typename T>
+__global__ void add_kernel(T* y, const T* x, long long n, float alpha) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    y[i] = from_f<T>(to_f(y[i]) + alpha * to_f(x[i]));
+}
+__global__ void cast_kernel(const float* x, uint16_t* y, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    y[i] = from_f<bf16_t>(x[i]).x;
+}
+template <typename T>
+__global__ void gather_rows_kernel(const T* src, long long lds, const int32_t* idx, int n, int cols, T* dst,
+                                   long long ldd) {
+  const int r = blockIdx.x;
+  if (r >= n) return;
+  const long long s = (long long)idx[r] * lds;
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) dst[(long long)r * ldd + c] = src[s + c];
+}
+template <typename T>
+__global__ void scatter_add_rows_kernel(const T* src, long long lds, const int32_t* idx, int n, int cols, T* dst,
+                                        long long ldd) {
+  const int r = blockIdx.x;
+  if (r >= n) return;
+  const long long d = (long long)idx[r] * ldd;
+  for (int c = threadIdx.x; c < cols; c += blockDim.x)
+    dst[d + c] = from_f<T>(to_f(dst[d + c]) + to_f(src[(long long)r * lds + c]));
+}
+
+int grid_for(long long n) { return (int)std::min<long long>((n + 255) / 256, 4096); }
+
+}  // namespace
+
+#define DISPATCH_T(dtype, ...)            \
+  if ((dtype) == K3M_F32) {               \
+    using T = float;                      \
+    __VA_ARGS__;                          \
+  } else if ((dtype) == K3M_BF16) {       \
+    using T = bf16_t;                     \
+    __VA_ARGS__;                          \
+  } else {                                \
+    return K3M_EINVAL;                    \
+  }
+
+extern "C" int k3m_ln_fwd(const void* x, const void* res, const float* gamma, const float* beta, void* y, void* xhat,
+                          float* rstd, int rows, int cols, float eps, float p_in, float p_out, uint64_t seed,
+                          uint64_t off_in, uint64_t off_out, int dtype, hipStream_t st) {
+  K3M_ARG(x && gamma && beta && y && rows >= 0 && cols % 256 == 0 && cols <= 1024 && cols > 0);
+  if (rows == 0) return 0;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ln_fwd_kernel<T>, dim3(k3m_cdiv(rows, 4)), dim3(256), 0, st,
+                                       (const T*)x, (const T*)res, gamma, beta, (T*)y, (T*)xhat, rstd, rows, cols, eps,
+                                       p_in, p_out, seed, off_in, off_out));
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_ln_bwd(const void* dy, const void* xhat, const float* rstd, const float* gamma, void* dres, void* dx,
+                          float* dgamma, float* dbeta, int rows, int cols, float p_in, float p_out, uint64_t seed,
+                          uint64_t off_in, uint64_t off_out, int acc_res, float* ws, int dtype, hipStream_t st) {
+  K3M_ARG(dy && xhat && rstd && gamma && dres && dx && dgamma && dbeta && ws);
+  K3M_ARG(cols % 256 == 0 && cols <= 1024 && rows >= 0);
+  if (rows == 0) return 0;
+  const int nb = std::min(LN_BWD_BLOCKS, k3m_cdiv(rows, 4));
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3(nb), dim3(256), 0, st, (const T*)dy, (const T*)xhat, rstd,
+                                       gamma, (T*)dres, (T*)dx, ws, rows, cols, p_in, p_out, seed, off_in, off_out,
+                                       acc_res));
+  K3M_CHECK_LAUNCH();
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(k3m_cdiv(cols, 256)), dim3(256), 0, st, ws, nb, cols, dgamma, 1);
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(k3m_cdiv(cols, 256)), dim3(256), 0, st, ws + (long long)nb * cols, nb, cols,
+                     dbeta, 1);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_embed_fwd(const int64_t* ids, const int64_t* tt, const float* word, const float* pos,
+                             const float* type, const float* gamma, const float* beta, void* y0, void* y1, void* y2,
+                             void* xhat, float* rstd, int nseq, int len, int hidden, float eps, float p_out,
+                             uint64_t seed, uint64_t off, int dtype, hipStream_t st) {
+  K3M_ARG(ids && tt && word && pos && type && gamma && beta && y0 && xhat && rstd);
+  K3M_ARG(hidden % 256 == 0 && hidden <= 1024);
+  const int rows = nseq * len;
+  if (rows == 0) return 0;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(embed_fwd_kernel<T>, dim3(k3m_cdiv(rows, 4)), dim3(256), 0, st, ids, tt, word,
+                                       pos, type, gamma, beta, (T*)y0, (T*)y1, (T*)y2, (T*)xhat, rstd, rows, len,
+                                       hidden, eps, p_out, seed, off));
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_embed_bwd(const int64_t* ids, const int64_t* tt, const void* ds, float* dword, float* dpos,
+                             float* dtype_, int nseq, int len, int hidden, int dtype, hipStream_t st) {
+  K3M_ARG(ids && tt && ds && dword && dpos && dtype_);
+  const int rows = nseq * len;
+  if (rows == 0) return 0;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(embed_bwd_kernel<T>, dim3(k3m_cdiv(rows, 4)), dim3(256), 0, st, ids, tt,
+                                       (const T*)ds, dword, dpos, dtype_, rows, len, hidden));
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_colsum(const void* x, long long ld, int rows, int cols, float* out, int accumulate, float* ws,
+                          int dtype, hipStream_t st) {
+  K3M_ARG(x && out && ws && rows >= 0 && cols >= 0);
+  if (cols == 0) return 0;
+  const int chunks = std::max(1, std::min(64, k3m_cdiv(rows, 64)));
+  DISPATCH_T(dtype, hipLaunchKernelGGL(colsum_kernel<T>, dim3(k3m_cdiv(cols, 256), chunks), dim3(256), 0, st,
+                                       (const T*)x, ld, rows, cols, ws));
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(k3m_cdiv(cols, 256)), dim3(256), 0, st, ws, chunks, cols, out, accumulate);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_dgelu(const void* g, const void* pre, void* out, long long n, int dtype, hipStream_t st) {
+  K3M_ARG(g && pre && out);
+  if (n == 0) return 0;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(dgelu_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, (const T*)g,
+                                       (const T*)pre, (T*)out, n));
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_add_inplace(void* y, const void* x, long long n, float alpha, int dtype, hipStream_t st) {
+  K3M_ARG(y && x);
+  if (n == 0) return 0;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(add_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, (T*)y, (const T*)x, n,
+                                       alpha));
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_cast_f32_bf16(const float* x, uint16_t* y, long long n, hipStream_t st) {
+  K3M_ARG(x && y);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(cast_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, y, n);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_gather_rows(const void* src, long long lds, const int32_t* idx, int n, int cols, void* dst,
+                               long long ldd, int dtype, hipStream_t st) {
+  K3M_ARG(src && idx && dst && n >= 0);
+  if (n == 0) return 0;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(gather_rows_kernel<T>, dim3(n), dim3(256), 0, st, (const T*)src, lds, idx, n,
+                                       cols, (T*)dst, ldd));
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_scatter_add_rows(const void* src, long long lds, const int32_t* idx, int n, int cols, void* dst,
+                                    long long ldd, int dtype, hipStream_t st) {
+  K3M_ARG(src && idx && dst && n >= 0);
+  if (n == 0) return 0;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(scatter_add_rows_kernel<T>, dim3(n), dim3(256), 0, st, (const T*)src, lds, idx,
+                                       n, cols, (T*)dst, ldd));
+  K3M_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,414 @@
+// Structure aggregator + link-prediction (LPM) loss, vectorised over a padded [B, NPV] triple
+// layout (reference: structure_aggregator, vilbert_k3m.py:2413-2505, a Python loop with one host
+// sync per triple).  Every item's triples are independent workgroups; the data-dependent parts
+// (number of valid triples, zero-triple items, negative draws) are index tables on the device.
+//
+// Semantics kept from the reference:
+//  * p_ij / v_ij = mean of the two ENDPOINT rows index_p[i,j] / index_v[i,j] (:2443-2444);
+//  * triples stop at the first j with index_p[i,j,0] == 0 (:2441);
+//  * an item without triples reuses the `t` of the latest earlier item that had triples, or
+//    [c_initial_0] if none did (bare except, :2452-2456)  -> src[i];
+//  * c_final_i = c_init_i + W3 (sum_j att_j t_j) + b3, att = softmax_j(w2.leaky_relu(t_j) + b2);
+//  * LPM: MarginRankingLoss(margin)(pos, neg, y=+1) = mean(max(0, neg - pos + margin)) (:2501).
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+__device__ __forceinline__ int count_valid(const int64_t* index_p, int i, int npv) {
+  int n = npv;
+  for (int j = 0; j < npv; ++j)
+    if (index_p[((long long)i * npv + j) * 2] == 0) {
+      n = j;
+      break;
+    }
+  return n;
+}
+
+__global__ void sa_count_kernel(const int64_t* index_p, int batch, int npv, int32_t* nvalid, int32_t* src) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  int last = -1;
+  for (int i = 0; i < batch; ++i) {
+    const int n = count_valid(index_p, i, npv);
+    nvalid[i] = n;
+    if (n > 0) {
+      src[i] = i;
+      last = i;
+    } else {
+      src[i] = last;  // -1 -> c_initial[0]
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void sa_gather_kernel(const T* seq, const int64_t* index_p, const int64_t* index_v,
+                                                       const float* c_init, float* X, const int32_t* nvalid, int len,
+                                                       int npv, int h) {
+  const int i = blockIdx.x / npv, j = blockIdx.x % npv;
+  float* x = X + (long long)blockIdx.x * 3 * h;
+  const bool ok = j < nvalid[i];
+  const long long ip = ((long long)i * npv + j) * 2;
+  const long long pa = ok ? index_p[ip] : 0, pb = ok ? index_p[ip + 1] : 0;
+  const long long va = ok ? index_v[ip] : 0, vb = ok ? index_v[ip + 1] : 0;
+  const T* s = seq + (long long)i * len * h;
+  for (int c = threadIdx.x; c < h; c += NT) {
+    if (ok) {
+      x[c] = c_init[(long long)i * h + c];
+      x[h + c] = (to_f(s[pa * h + c]) + to_f(s[pb * h + c])) * 0.5f;
+      x[2 * h + c] = (to_f(s[va * h + c]) + to_f(s[vb * h + c])) * 0.5f;
+    } else {
+      x[c] = 0.f;
+      x[h + c] = 0.f;
+      x[2 * h + c] = 0.f;
+    }
+  }
+}
+
+__device__ __forceinline__ float lrelu(float x) { return x > 0.f ? x : 0.01f * x; }
+
+// one workgroup per item; npv <= 64
+__global__ __launch_bounds__(NT) void sa_attn_fwd_kernel(const float* T, const int32_t* nvalid, const int32_t* src,
+                                                         const float* w2, const float* b2, const float* c_init,
+                                                         float* att, float* agg, int npv, int h) {
+  __shared__ float red[4];
+  __shared__ float beta_s[64];
+  const int i = blockIdx.x;
+  const int s = src[i];
+  float* ag = agg + (long long)i * h;
+  float* at = att + (long long)i * npv;
+  if (s < 0) {
+    for (int c = threadIdx.x; c < h; c += NT) ag[c] = c_init[c];
+    for (int j = threadIdx.x; j < npv; j += NT) at[j] = j == 0 ? 1.f : 0.f;
+    return;
+  }
+  const int n = nvalid[s];
+  for (int j = 0; j < n; ++j) {
+    const float* t = T + ((long long)s * npv + j) * h;
+    float a = 0.f;
+    for (int c = threadIdx.x; c < h; c += NT) a += w2[c] * lrelu(t[c]);
+    a = block_sum<4>(a, red);
+    if (threadIdx.x == 0) beta_s[j] = a + b2[0];
+  }
+  __syncthreads();
+  float mx = -INFINITY;
+  for (int j = 0; j < n; ++j) mx = fmaxf(mx, beta_s[j]);
+  float sum = 0.f;
+  for (int j = 0; j < n; ++j) sum += expf(beta_s[j] - mx);
+  for (int j = threadIdx.x; j < npv; j += NT) at[j] = j < n ? expf(beta_s[j] - mx) / sum : 0.f;
+  for (int c = threadIdx.x; c < h; c += NT) {
+    float a = 0.f;
+    for (int j = 0; j < n; ++j) a += (expf(beta_s[j] - mx) / sum) * T[((long long)s * npv + j) * h + c];
+    ag[c] = a;
+  }
+}
+
+__global__ __launch_bounds__(NT) void sa_attn_bwd_kernel(const float* dagg, const float* T, const float* att,
+                                                         const int32_t* nvalid, const int32_t* src, const float* w2,
+                                                         float* dT, float* dw2, float* db2, float* dc_init, int npv,
+                                                         int h) {
+  __shared__ float red[4];
+  __shared__ float datt[64];
+  const int i = blockIdx.x;
+  const int s = src[i];
+  const float* dg = dagg + (long long)i * h;
+  if (s < 0) {
+    for (int c = threadIdx.x; c < h; c += NT) atomicAdd(dc_init + c, dg[c]);
+    return;
+  }
+  const int n = nvalid[s];
+  const float* at = att + (long long)i * npv;
+  for (int j = 0; j < n; ++j) {
+    const float* t = T + ((long long)s * npv + j) * h;
+    float a = 0.f;
+    for (int c = threadIdx.x; c < h; c += NT) a += dg[c] * t[c];
+    a = block_sum<4>(a, red);
+    if (threadIdx.x == 0) datt[j] = a;
+  }
+  __syncthreads();
+  float dot = 0.f;
+  for (int j = 0; j < n; ++j) dot += at[j] * datt[j];
+  float db = 0.f;
+  for (int j = 0; j < n; ++j) {
+    const float dbeta = at[j] * (datt[j] - dot);
+    db += dbeta;
+    const float* t = T + ((long long)s * npv + j) * h;
+    float* dt = dT + ((long long)s * npv + j) * h;
+    for (int c = threadIdx.x; c < h; c += NT) {
+      const float tv = t[c];
+      const float g = at[j] * dg[c] + dbeta * w2[c] * (tv > 0.f ? 1.f : 0.01f);
+      atomicAdd(dt + c, g);
+      atomicAdd(dw2 + c, dbeta * lrelu(tv));
+    }
+  }
+  if (threadIdx.x == 0) atomicAdd(db2, db);
+}
+
+// pair p of triple (i, j): e = 0,1 entity negatives; e = 2,3 value negatives
+__device__ __forceinline__ bool pair_neg(const int64_t* ent, const int64_t* val, long long ij, int e, int& k) {
+  const long long v = e < 2 ? ent[ij * 2 + e] : val[ij * 2 + (e - 2)];
+  k = (int)v;
+  return v >= 0;
+}
+
+// ws layout: [B*npv*4] hinge (-1 = no pair), [B*npv] pos norm, [B*npv*4] neg norm, [2] (count, sum)
+__global__ __launch_bounds__(NT) void lpm_fwd_kernel(const float* cf, const float* X, const int32_t* nvalid,
+                                                     const int64_t* ent, const int64_t* val, int npv, int h,
+                                                     float margin, float* ws, int total) {
+  __shared__ float red[4];
+  const int i = blockIdx.x / npv, j = blockIdx.x % npv;
+  const long long ij = blockIdx.x;
+  float* hinge = ws;
+  float* posn = ws + (long long)total * 4;
+  float* negn = posn + total;
+  if (j >= nvalid[i]) {
+    if (threadIdx.x < 4) hinge[ij * 4 + threadIdx.x] = -1.f;
+    return;
+  }
+  const float* x = X + ij * 3 * h;
+  float a = 0.f;
+  for (int c = threadIdx.x; c < h; c += NT) {
+    const float u = cf[(long long)i * h + c] + x[h + c] - x[2 * h + c];
+    a += u * u;
+  }
+  const float pn = sqrtf(block_sum<4>(a, red));
+  if (threadIdx.x == 0) posn[ij] = pn;
+  for (int e = 0; e < 4; ++e) {
+    int k;
+    const bool has = pair_neg(ent, val, ij, e, k);
+    if (!has) {
+      if (threadIdx.x == 0) hinge[ij * 4 + e] = -1.f;
+      continue;
+    }
+    float b = 0.f;
+    for (int c = threadIdx.x; c < h; c += NT) {
+      float u;
+      if (e < 2) u = cf[(long long)k * h + c] + x[h + c] - x[2 * h + c];
+      else u = cf[(long long)i * h + c] + x[h + c] - X[((long long)i * npv + k) * 3 * h + 2 * h + c];
+      b += u * u;
+    }
+    const float nn = sqrtf(block_sum<4>(b, red));
+    if (threadIdx.x == 0) {
+      negn[ij * 4 + e] = nn;
+      hinge[ij * 4 + e] = fmaxf(0.f, nn - pn + margin);
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT) void lpm_reduce_kernel(float* ws, int total, float* loss) {
+  __shared__ float red[4];
+  float cnt = 0.f, sum = 0.f;
+  for (int p = threadIdx.x; p < total * 4; p += NT) {
+    const float hv = ws[p];
+    if (hv >= 0.f) {
+      cnt += 1.f;
+      sum += hv;
+    }
+  }
+  cnt = block_sum<4>(cnt, red);
+  sum = block_sum<4>(sum, red);
+  if (threadIdx.x == 0) {
+    float* tail = ws + (long long)total * 9;
+    tail[0] = cnt;
+    tail[1] = sum;
+    loss[0] = cnt > 0.f ? sum / cnt : NAN;  // mean of an empty tensor is NaN, as in the reference
+  }
+}
+
+__global__ __launch_bounds__(NT) void lpm_bwd_kernel(const float* cf, const float* X, const int32_t* nvalid,
+                                                     const int64_t* ent, const int64_t* val, int npv, int h,
+                                                     const float* ws, int total, float* dcf, float* dX) {
+  const int i = blockIdx.x / npv, j = blockIdx.x % npv;
+  const long long ij = blockIdx.x;
+  if (j >= nvalid[i]) return;
+  const float* hinge = ws;
+  const float* posn = ws + (long long)total * 4;
+  const float* negn = posn + total;
+  const float cnt = ws[(long long)total * 9];
+  const float w = 1.f / cnt;
+  const float* x = X + ij * 3 * h;
+  float* dx = dX + ij * 3 * h;
+  // coefficient of the positive norm: -w per active pair
+  float cpos = 0.f;
+  float cneg[4];
+  int kk[4];
+  for (int e = 0; e < 4; ++e) {
+    cneg[e] = 0.f;
+    kk[e] = -1;
+    int k;
+    if (pair_neg(ent, val, ij, e, k) && hinge[ij * 4 + e] > 0.f) {
+      cpos -= w;
+      cneg[e] = w / fmaxf(negn[ij * 4 + e], 1e-30f);
+      kk[e] = k;
+    }
+  }
+  const float cp = cpos / fmaxf(posn[ij], 1e-30f);
+  for (int c = threadIdx.x; c < h; c += NT) {
+    const float p = x[h + c], v = x[2 * h + c];
+    const float up = cf[(long long)i * h + c] + p - v;
+    float gci = cp * up, gp = cp * up, gv = -cp * up;
+    for (int e = 0; e < 4; ++e) {
+      if (kk[e] < 0) continue;
+      if (e < 2) {
+        const float u = cf[(long long)kk[e] * h + c] + p - v;
+        const float g = cneg[e] * u;
+        atomicAdd(dcf + (long long)kk[e] * h + c, g);
+        gp += g;
+        gv -= g;
+      } else {
+        const long long ik = (long long)i * npv + kk[e];
+        const float u = cf[(long long)i * h + c] + p - X[ik * 3 * h + 2 * h + c];
+        const float g = cneg[e] * u;
+        gci += g;
+        gp += g;
+        atomicAdd(dX + ik * 3 * h + 2 * h + c, -g);
+      }
+    }
+    atomicAdd(dcf + (long long)i * h + c, gci);
+    atomicAdd(dx + h + c, gp);
+    atomicAdd(dx + 2 * h + c, gv);
+  }
+}
+
+// reference draw: random.sample(candidates, min(len, n)) without replacement
+__global__ void lpm_sample_kernel(const int32_t* nvalid, int batch, int npv, int n_ent, int n_val, uint64_t seed,
+                                  uint64_t off, int64_t* ent, int64_t* val) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= batch * npv) return;
+  const int i = t / npv, j = t % npv;
+  ent[t * 2] = ent[t * 2 + 1] = -1;
+  val[t * 2] = val[t * 2 + 1] = -1;
+  const int n = nvalid[i];
+  if (j >= n) return;
+  const uint64_t base = off + (uint64_t)t * 4;
+  // entity candidates: all k != i
+  {
+    const int nc = batch - 1, take = min(nc, min(n_ent, 2));
+    int first = -1;
+    for (int q = 0; q < take; ++q) {
+      const int m = nc - q;
+      int r = (int)(k3m_hash(seed, base + q) % (uint32_t)m);
+      if (q == 1 && r >= first) r += 1;  // skip the already drawn candidate rank
+      if (q == 0) first = r;
+      const int k = r >= i ? r + 1 : r;  // rank among candidates -> item index
+      ent[t * 2 + q] = k;
+    }
+  }
+  {
+    const int nc = n - 1, take = min(nc, min(n_val, 2));
+    int first = -1;
+    for (int q = 0; q < take; ++q) {
+      const int m = nc - q;
+      int r = (int)(k3m_hash(seed, base + 2 + q) % (uint32_t)m);
+      if (q == 1 && r >= first) r += 1;
+      if (q == 0) first = r;
+      val[t * 2 + q] = r >= j ? r + 1 : r;
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void sa_gather_bwd_kernel(const float* dX, const int64_t* index_p,
+                                                           const int64_t* index_v, const int32_t* nvalid, T* dseq,
+                                                           float* dc_init, int len, int npv, int h) {
+  const int i = blockIdx.x / npv, j = blockIdx.x % npv;
+  if (j >= nvalid[i]) return;
+  const long long ip = ((long long)i * npv + j) * 2;
+  const long long pa = index_p[ip], pb = index_p[ip + 1], va = index_v[ip], vb = index_v[ip + 1];
+  const float* dx = dX + (long long)blockIdx.x * 3 * h;
+  T* ds = dseq + (long long)i * len * h;
+  for (int c = threadIdx.x; c < h; c += NT) {
+    atomicAdd(dc_init + (long long)i * h + c, dx[c]);
+    const float gp = 0.5f * dx[h + c], gv = 0.5f * dx[2 * h + c];
+    atomicAdd(reinterpret_cast<float*>(ds) + pa * h + c, gp);
+    atomicAdd(reinterpret_cast<float*>(ds) + pb * h + c, gp);
+    atomicAdd(reinterpret_cast<float*>(ds) + va * h + c, gv);
+    atomicAdd(reinterpret_cast<float*>(ds) + vb * h + c, gv);
+  }
+}
+
+}  // namespace
+
+extern "C" int k3m_sa_gather(const void* seq, const int64_t* index_p, const int64_t* index_v, const float* c_init,
+                             float* X, int32_t* nvalid, int32_t* src, int batch, int len, int npv, int hidden,
+                             int dtype, hipStream_t st) {
+  K3M_ARG(seq && index_p && index_v && c_init && X && nvalid && src && npv > 0 && npv <= 64);
+  K3M_ARG(dtype == K3M_F32);
+  if (batch == 0) return 0;
+  hipLaunchKernelGGL(sa_count_kernel, dim3(1), dim3(64), 0, st, index_p, batch, npv, nvalid, src);
+  hipLaunchKernelGGL(sa_gather_kernel<float>, dim3(batch * npv), dim3(NT), 0, st, (const float*)seq, index_p, index_v,
+                     c_init, X, nvalid, len, npv, hidden);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_sa_attn_fwd(const float* T, const int32_t* nvalid, const int32_t* src, const float* w2,
+                               const float* b2, const float* c_init, float* att, float* agg, int batch, int npv,
+                               int hidden, hipStream_t st) {
+  K3M_ARG(T && nvalid && src && w2 && b2 && c_init && att && agg && npv <= 64);
+  if (batch == 0) return 0;
+  hipLaunchKernelGGL(sa_attn_fwd_kernel, dim3(batch), dim3(NT), 0, st, T, nvalid, src, w2, b2, c_init, att, agg, npv,
+                     hidden);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_sa_attn_bwd(const float* dagg, const float* T, const float* att, const int32_t* nvalid,
+                               const int32_t* src, const float* w2, float* dT, float* dw2, float* db2, float* dc_init,
+                               int batch, int npv, int hidden, hipStream_t st) {
+  K3M_ARG(dagg && T && att && nvalid && src && w2 && dT && dw2 && db2 && dc_init && npv <= 64);
+  if (batch == 0) return 0;
+  hipLaunchKernelGGL(sa_attn_bwd_kernel, dim3(batch), dim3(NT), 0, st, dagg, T, att, nvalid, src, w2, dT, dw2, db2,
+                     dc_init, npv, hidden);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_lpm_fwd(const float* c_final, const float* X, const int32_t* nvalid, const int64_t* ent_neg,
+                           const int64_t* val_neg, int batch, int npv, int hidden, float margin, float* loss, float* ws,
+                           hipStream_t st) {
+  K3M_ARG(c_final && X && nvalid && ent_neg && val_neg && loss && ws);
+  const int total = batch * npv;
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(lpm_fwd_kernel, dim3(total), dim3(NT), 0, st, c_final, X, nvalid, ent_neg, val_neg, npv, hidden,
+                     margin, ws, total);
+  hipLaunchKernelGGL(lpm_reduce_kernel, dim3(1), dim3(NT), 0, st, ws, total, loss);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_lpm_bwd(const float* c_final, const float* X, const int32_t* nvalid, const int64_t* ent_neg,
+                           const int64_t* val_neg, int batch, int npv, int hidden, float margin, const float* ws,
+                           float* dc_final, float* dX, hipStream_t st) {
+  K3M_ARG(c_final && X && nvalid && ent_neg && val_neg && ws && dc_final && dX);
+  (void)margin;
+  const int total = batch * npv;
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(lpm_bwd_kernel, dim3(total), dim3(NT), 0, st, c_final, X, nvalid, ent_neg, val_neg, npv, hidden,
+                     ws, total, dc_final, dX);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_lpm_sample(const int32_t* nvalid, int batch, int npv, int n_ent, int n_val, uint64_t seed,
+                              uint64_t off, int64_t* ent_neg, int64_t* val_neg, hipStream_t st) {
+  K3M_ARG(nvalid && ent_neg && val_neg);
+  const int total = batch * npv;
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(lpm_sample_kernel, dim3(k3m_cdiv(total, 256)), dim3(256), 0, st, nvalid, batch, npv, n_ent, n_val,
+                     seed, off, ent_neg, val_neg);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_sa_gather_bwd(const float* dX, const int64_t* index_p, const int64_t* index_v,
+                                 const int32_t* nvalid, void* dseq, float* dc_init, int batch, int len, int npv,
+                                 int hidden, int dtype, hipStream_t st) {
+  K3M_ARG(dX && index_p && index_v && nvalid && dseq && dc_init);
+  K3M_ARG(dtype == K3M_F32);
+  if (batch == 0) return 0;
+  hipLaunchKernelGGL(sa_gather_bwd_kernel<float>, dim3(batch * npv), dim3(NT), 0, st, dX, index_p, index_v, nvalid,
+                     (float*)dseq, dc_init, len, npv, hidden);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}

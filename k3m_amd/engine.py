@@ -1,0 +1,783 @@
+"""K3M tri-modal pretraining step on MI355X: forward + explicit backward over libk3m_hip kernels.
+
+Reference: BertForMultiModalPreTraining_tri_stru (vilbert_k3m/vilbert_k3m.py:2186-2859) driven by
+train_concap_struc.py:466-589.
+
+MI355X-first organisation ("wide" passes)
+-----------------------------------------
+The reference runs three independent pair passes (calculate_for_text_img :1154,
+calculate_for_pv_img :1332, calculate_for_two_text :1510) that each re-run the SHARED 12 text
+layers and 6 image layers.  The layer index is in lock-step across the passes (every pass runs
+text layers [t_start, t_end) and image layers [v_start, v_end) before co-attention block c), so
+this engine stacks the streams of all passes row-wise and runs each shared layer ONCE per step:
+
+    wide text buffer  [2B*T + 2B*P, 768] = [text(p1) | text(p3) | pv(p2) | pv(p3)]
+    wide image buffer [2B*R, 1024]       = [img(p1)  | img(p2)]
+
+One text-layer launch then covers 20,992 rows at bs=64 (4x fewer, 4x larger GEMMs than the
+reference), and each weight gradient is one GEMM reducing over every use of the weight.
+Co-attention block c applies the three pass-specific layers (c_layer, c_layer_pv_v,
+c_layer_pv_t) to disjoint row slices.  Dropout masks are per row, so stacking is exact.
+
+Parameters and gradients live in one flat fp32 buffer each (k3m_amd/params.py); weight
+gradients are accumulated in place by the GEMM epilogue (beta = 1) and bias/LN gradients by the
+reduction kernels, so there is no autograd bookkeeping on the hot path.
+"""
+import math
+
+import torch
+
+from . import _lib as L
+from . import ops
+from .params import flat_layout
+
+EPS = 1e-12
+
+
+class Rng(object):
+    """Counter-based RNG bookkeeping: each random site gets (seed, offset) and the backward pass
+    regenerates its draws from the same pair."""
+
+    def __init__(self, seed):
+        self.seed = int(seed) & ((1 << 63) - 1)
+        self.off = 0
+
+    def take(self, n):
+        o = self.off
+        self.off += int(n)
+        return o
+
+
+class FlatParams(object):
+    """All parameters (and their gradients) as views into single contiguous fp32 buffers."""
+
+    def __init__(self, cfg, device):
+        self.spec, self.offsets, self.segments, self.total, self.shapes = flat_layout(cfg)
+        self.device = device
+        self.data = torch.zeros(self.total, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(self.total, dtype=torch.float32, device=device)
+        self.p, self.g = {}, {}
+        for name, shape in self.spec:
+            o = self.offsets[name]
+            n = math.prod(shape)
+            self.p[name] = self.data[o:o + n].view(shape)
+            self.g[name] = self.grad[o:o + n].view(shape)
+
+    def fused(self, names, grad=False):
+        """Contiguous view spanning adjacent tensors (e.g. query|key|value weights -> [3H, H])."""
+        buf = self.grad if grad else self.data
+        o = self.offsets[names[0]]
+        n = 0
+        for nm in names:
+            assert self.offsets[nm] == o + n, "tensors are not adjacent: %s" % nm
+            n += math.prod(self.shapes[nm])
+        sh0 = self.shapes[names[0]]
+        rows = sum(self.shapes[nm][0] for nm in names)
+        return buf[o:o + n].view((rows,) + tuple(sh0[1:]))
+
+    def load(self, values):
+        for name, _ in self.spec:
+            v = values[name]
+            t = torch.as_tensor(v) if not isinstance(v, torch.Tensor) else v
+            self.p[name].copy_(t.to(torch.float32).reshape(self.shapes[name]))
+
+    def state_dict(self):
+        sd = {}
+        for name, _ in self.spec:
+            sd[name] = self.p[name]
+        sd["cls.predictions.decoder.weight"] = self.p["embeddings.word_embeddings.weight"]
+        return sd
+
+
+class Lin(object):
+    """A (possibly fused) Linear: weight [N,K] / bias [N] views + gradient views."""
+
+    def __init__(self, fp, prefixes):
+        if isinstance(prefixes, str):
+            prefixes = [prefixes]
+        w = [p + ".weight" for p in prefixes]
+        b = [p + ".bias" for p in prefixes]
+        self.W, self.gW = fp.fused(w), fp.fused(w, True)
+        self.b, self.gb = fp.fused(b), fp.fused(b, True)
+
+    def fwd(self, x, out=None, epi=None, aux=None, alpha=1.0, beta=0.0):
+        return ops.linear(x, self.W, self.b, out=out, epi=epi, aux=aux, alpha=alpha, beta=beta)
+
+    def wgrad(self, dy, x, alpha=1.0):
+        ops.linear_wgrad(dy, x, self.gW, self.gb, alpha=alpha)
+
+    def dgrad(self, dy, dx=None, beta=0.0, dgelu_aux=None, alpha=1.0):
+        return ops.linear_dgrad(dy, self.W, dx=dx, beta=beta, dgelu_aux=dgelu_aux, alpha=alpha)
+
+
+class LN(object):
+    def __init__(self, fp, prefix):
+        self.g, self.b = fp.p[prefix + ".weight"], fp.p[prefix + ".bias"]
+        self.gg, self.gb = fp.g[prefix + ".weight"], fp.g[prefix + ".bias"]
+
+
+# ---------------------------------------------------------------- sub-blocks
+
+class AddLN(object):
+    """y = LN(dropout(x) + res) (BertSelfOutput / BertOutput / BertBiOutput tails)."""
+
+    def __init__(self, ln, p):
+        self.ln, self.p = ln, p
+
+    def fwd(self, x, res, rng, out=None):
+        M, H = x.shape
+        y = out if out is not None else torch.empty_like(x)
+        xhat = torch.empty((M, H), dtype=x.dtype, device=x.device)
+        rstd = torch.empty((M,), dtype=torch.float32, device=x.device)
+        off = rng.take(M * H) if self.p > 0 else 0
+        ops.ln_fwd(x, res, self.ln.g, self.ln.b, y, xhat, rstd, p_in=self.p, seed=rng.seed, off_in=off)
+        return y, (xhat, rstd, rng.seed, off)
+
+    def bwd(self, dy, saved, dres):
+        """writes d(res) into dres; returns d(x) (aliases dres when dropout is off)."""
+        xhat, rstd, seed, off = saved
+        dx = dres if self.p == 0 else torch.empty_like(dres)
+        ops.ln_bwd(dy, xhat, rstd, self.ln.g, dres, dx, self.ln.gg, self.ln.gb, p_in=self.p, seed=seed, off_in=off)
+        return dx
+
+
+class FFN(object):
+    """BertIntermediate(gelu) + BertOutput (post-LN), vilbert_k3m.py:504-532 / :665-693."""
+
+    def __init__(self, fp, inter, outp, p):
+        self.i = Lin(fp, inter + ".dense")
+        self.o = Lin(fp, outp + ".dense")
+        self.tail = AddLN(LN(fp, outp + ".LayerNorm"), p)
+
+    def fwd(self, h, rng, out=None):
+        M = h.shape[0]
+        I = self.i.W.shape[0]
+        u = torch.empty((M, I), dtype=h.dtype, device=h.device)
+        f = self.i.fwd(h, epi=L.EPI_BIAS_GELU, aux=u)
+        o = self.o.fwd(f)
+        y, tsv = self.tail.fwd(o, h, rng, out=out)
+        return y, (h, u, f, tsv)
+
+    def bwd(self, dy, saved, dh_out=None):
+        h, u, f, tsv = saved
+        dh = dh_out if dh_out is not None else torch.empty_like(h)
+        do = self.tail.bwd(dy, tsv, dh)
+        self.o.wgrad(do, f)
+        du = self.o.dgrad(do, dgelu_aux=u)
+        self.i.wgrad(du, h)
+        self.i.dgrad(du, dx=dh, beta=1.0)
+        return dh
+
+
+def _attn_fwd(q, k, v, mask, nseq, lq, lk, nh, p, rng, out=None):
+    hd = q.shape[1] // nh
+    ctx = out if out is not None else torch.empty((nseq * lq, q.shape[1]), dtype=q.dtype, device=q.device)
+    probs = torch.empty((nseq * nh * lq * lk,), dtype=torch.float32, device=q.device)
+    off = rng.take(probs.numel()) if p > 0 else 0
+    ops.attn_fwd(q, k, v, mask, ctx, probs, nseq, lq, lk, nh, hd, 1.0 / math.sqrt(hd), p, rng.seed, off)
+    return ctx, (probs, nseq, lq, lk, nh, hd, p, rng.seed, off)
+
+
+def _attn_bwd(dctx, q, k, v, saved, dq, dk, dv):
+    probs, nseq, lq, lk, nh, hd, p, seed, off = saved
+    ops.attn_bwd(dctx, q, k, v, probs, dq, dk, dv, nseq, lq, lk, nh, hd, 1.0 / math.sqrt(hd), p, seed, off)
+
+
+class BertLayerOp(object):
+    """BertLayer / BertImageLayer (vilbert_k3m.py:535-548, :696-709) over a wide buffer whose rows
+    hold several sequence segments [(row0, nseq, L, mask)]."""
+
+    def __init__(self, fp, prefix, nh, p_attn, p_hidden):
+        self.qkv = Lin(fp, [prefix + ".attention.self.query", prefix + ".attention.self.key",
+                            prefix + ".attention.self.value"])
+        self.o = Lin(fp, prefix + ".attention.output.dense")
+        self.tail = AddLN(LN(fp, prefix + ".attention.output.LayerNorm"), p_hidden)
+        self.ffn = FFN(fp, prefix + ".intermediate", prefix + ".output", p_hidden)
+        self.nh, self.p_attn = nh, p_attn
+
+    def fwd(self, x, segs, rng):
+        M, H = x.shape
+        qkv = self.qkv.fwd(x)
+        ctx = torch.empty((M, H), dtype=x.dtype, device=x.device)
+        asv = []
+        for (r0, nseq, ln, mask) in segs:
+            r1 = r0 + nseq * ln
+            _, s = _attn_fwd(qkv[r0:r1, 0:H], qkv[r0:r1, H:2 * H], qkv[r0:r1, 2 * H:], mask, nseq, ln, ln, self.nh,
+                             self.p_attn, rng, out=ctx[r0:r1])
+            asv.append(s)
+        a = self.o.fwd(ctx)
+        h1, tsv = self.tail.fwd(a, x, rng)
+        y, fsv = self.ffn.fwd(h1, rng)
+        return y, (x, qkv, ctx, asv, tsv, fsv, segs)
+
+    def bwd(self, dy, saved):
+        x, qkv, ctx, asv, tsv, fsv, segs = saved
+        M, H = x.shape
+        dh1 = self.ffn.bwd(dy, fsv)
+        dx = torch.empty_like(x)
+        da = self.tail.bwd(dh1, tsv, dx)
+        self.o.wgrad(da, ctx)
+        dctx = self.o.dgrad(da)
+        dqkv = torch.empty_like(qkv)
+        for (r0, nseq, ln, mask), s in zip(segs, asv):
+            r1 = r0 + nseq * ln
+            _attn_bwd(dctx[r0:r1], qkv[r0:r1, 0:H], qkv[r0:r1, H:2 * H], qkv[r0:r1, 2 * H:], s,
+                      dqkv[r0:r1, 0:H], dqkv[r0:r1, H:2 * H], dqkv[r0:r1, 2 * H:])
+        self.qkv.wgrad(dqkv, x)
+        self.qkv.dgrad(dqkv, dx=dx, beta=1.0)
+        return dx
+
+
+class ConnectionOp(object):
+    """BertConnectionLayer / BertConnectionLayer_two_text (vilbert_k3m.py:1030-1111):
+    bi-directional attention between stream 1 (image or PV) and stream 2 (text or PV)."""
+
+    def __init__(self, fp, prefix, nh, p_attn1, p_attn2, p_h1, p_h2, p_ffn1, p_ffn2):
+        b = prefix + ".biattention."
+        self.qkv1 = Lin(fp, [b + "query1", b + "key1", b + "value1"])
+        self.qkv2 = Lin(fp, [b + "query2", b + "key2", b + "value2"])
+        o = prefix + ".biOutput."
+        self.d1, self.d2 = Lin(fp, o + "dense1"), Lin(fp, o + "dense2")
+        self.t1 = AddLN(LN(fp, o + "LayerNorm1"), p_h1)
+        self.t2 = AddLN(LN(fp, o + "LayerNorm2"), p_h2)
+        self.f1 = FFN(fp, prefix + ".v_intermediate", prefix + ".v_output", p_ffn1)
+        self.f2 = FFN(fp, prefix + ".t_intermediate", prefix + ".t_output", p_ffn2)
+        self.nh, self.pa1, self.pa2 = nh, p_attn1, p_attn2
+
+    def fwd(self, s1, s2, nseq, l1, l2, mask1, mask2, rng, out1, out2):
+        Hb = self.qkv1.W.shape[0] // 3
+        q1 = self.qkv1.fwd(s1)
+        q2 = self.qkv2.fwd(s2)
+        # ctx1: stream-2 queries over stream-1 keys (+ stream-1 mask); ctx2 the converse (:786-824)
+        ctx1, a1s = _attn_fwd(q2[:, 0:Hb], q1[:, Hb:2 * Hb], q1[:, 2 * Hb:], mask1, nseq, l2, l1, self.nh, self.pa1, rng)
+        ctx2, a2s = _attn_fwd(q1[:, 0:Hb], q2[:, Hb:2 * Hb], q2[:, 2 * Hb:], mask2, nseq, l1, l2, self.nh, self.pa2, rng)
+        h1, t1s = self.t1.fwd(self.d1.fwd(ctx2), s1, rng)
+        h2, t2s = self.t2.fwd(self.d2.fwd(ctx1), s2, rng)
+        _, f1s = self.f1.fwd(h1, rng, out=out1)
+        _, f2s = self.f2.fwd(h2, rng, out=out2)
+        return (s1, s2, q1, q2, ctx1, ctx2, a1s, a2s, t1s, t2s, f1s, f2s, Hb)
+
+    def bwd(self, dy1, dy2, saved, ds1, ds2):
+        s1, s2, q1, q2, ctx1, ctx2, a1s, a2s, t1s, t2s, f1s, f2s, Hb = saved
+        dh1 = self.f1.bwd(dy1, f1s)
+        dh2 = self.f2.bwd(dy2, f2s)
+        da1 = self.t1.bwd(dh1, t1s, ds1)
+        da2 = self.t2.bwd(dh2, t2s, ds2)
+        self.d1.wgrad(da1, ctx2)
+        dctx2 = self.d1.dgrad(da1)
+        self.d2.wgrad(da2, ctx1)
+        dctx1 = self.d2.dgrad(da2)
+        dq1 = torch.empty_like(q1)
+        dq2 = torch.empty_like(q2)
+        _attn_bwd(dctx1, q2[:, 0:Hb], q1[:, Hb:2 * Hb], q1[:, 2 * Hb:], a1s, dq2[:, 0:Hb], dq1[:, Hb:2 * Hb],
+                  dq1[:, 2 * Hb:])
+        _attn_bwd(dctx2, q1[:, 0:Hb], q2[:, Hb:2 * Hb], q2[:, 2 * Hb:], a2s, dq1[:, 0:Hb], dq2[:, Hb:2 * Hb],
+                  dq2[:, 2 * Hb:])
+        self.qkv1.wgrad(dq1, s1)
+        self.qkv1.dgrad(dq1, dx=ds1, beta=1.0)
+        self.qkv2.wgrad(dq2, s2)
+        self.qkv2.dgrad(dq2, dx=ds2, beta=1.0)
+
+
+def _ext_mask(m):
+    # (1 - mask) * -10000 additive key mask (vilbert_k3m.py:2547-2580); input marshalling
+    return ((1.0 - m.to(torch.float32)) * -10000.0).contiguous()
+
+
+class K3MEngine(object):
+    """One replica of the model on one GPU (one process per GPU; DDP in k3m_amd/ddp.py)."""
+
+    def __init__(self, cfg, device=None, seed=1234):
+        self.cfg = cfg
+        self.device = torch.device(device if device is not None else "cuda")
+        L.load()
+        fp = self.fp = FlatParams(cfg, self.device)
+        self.base_seed = int(seed)
+        self.step_count = 0
+        c = cfg
+        assert getattr(c, "fixed_t_layer", 0) == 0 and getattr(c, "fixed_v_layer", 0) == 0
+        assert not getattr(c, "in_batch_pairs", False) and not getattr(c, "fast_mode", False)
+        assert not getattr(c, "dynamic_attention", False) and getattr(c, "model", "bert") == "bert"
+        assert getattr(c, "use_image", True) and c.with_coattention
+        assert getattr(c, "visual_target", 0) == 0
+        self.H, self.Hv, self.Hb = c.hidden_size, c.v_hidden_size, c.bi_hidden_size
+        self.p_h = c.hidden_dropout_prob
+        self.p_a = c.attention_probs_dropout_prob
+        self.p_vh = c.v_hidden_dropout_prob
+        self.p_va = c.v_attention_probs_dropout_prob
+        self.text = [BertLayerOp(fp, "encoder.layer.%d" % i, c.num_attention_heads, self.p_a, self.p_h)
+                     for i in range(c.num_hidden_layers)]
+        self.image = [BertLayerOp(fp, "encoder.v_layer.%d" % i, c.v_num_attention_heads, self.p_va, self.p_vh)
+                      for i in range(c.v_num_hidden_layers)]
+        nco = len(c.v_biattention_id)
+        nb = c.bi_num_attention_heads
+        self.co_tv = [ConnectionOp(fp, "encoder.c_layer.%d" % i, nb, self.p_va, self.p_a, self.p_vh, self.p_h,
+                                   self.p_vh, self.p_h) for i in range(nco)]
+        self.co_pv = [ConnectionOp(fp, "encoder.c_layer_pv_v.%d" % i, nb, self.p_va, self.p_a, self.p_vh, self.p_h,
+                                   self.p_vh, self.p_h) for i in range(nco)]
+        self.co_tt = [ConnectionOp(fp, "encoder.c_layer_pv_t.%d" % i, nb, self.p_va, self.p_a, self.p_vh, self.p_h,
+                                   self.p_h, self.p_h) for i in range(nco)]
+        self.emb_ln = LN(fp, "embeddings.LayerNorm")
+        self.vemb_img = Lin(fp, "v_embeddings.image_embeddings")
+        self.vemb_loc = Lin(fp, "v_embeddings.image_location_embeddings")
+        self.vemb_ln = LN(fp, "v_embeddings.LayerNorm")
+        self.gate = {m: Lin(fp, ["score_self_%s" % m, "score_cross1_%s" % m, "score_cross2_%s" % m])
+                     for m in ("v", "t", "pv")}
+        self.map_b2i = Lin(fp, "map_bi_to_individual")
+        self.mlm_t = Lin(fp, "cls.predictions.transform.dense")
+        self.mlm_ln = LN(fp, "cls.predictions.transform.LayerNorm")
+        self.img_t = Lin(fp, "cls.imagePredictions.transform.dense")
+        self.img_ln = LN(fp, "cls.imagePredictions.transform.LayerNorm")
+        self.img_dec = Lin(fp, "cls.imagePredictions.decoder")
+        self.sw1, self.sw3 = Lin(fp, "struc_w1"), Lin(fp, "struc_w3")
+        self.schedule = self._schedule()
+
+    # ------------------------------------------------------------ encoder schedule
+    def _schedule(self):
+        """[(kind, index)] in lock-step order: ('t', i) text layer on all four text/PV streams,
+        ('v', i) image layer on both image streams, ('c', i) co-attention block i."""
+        c = self.cfg
+        sch = []
+        t0 = v0 = 0
+        for i, (v1, t1) in enumerate(zip(c.v_biattention_id, c.t_biattention_id)):
+            sch += [("t", k) for k in range(t0, t1)]
+            sch += [("v", k) for k in range(v0, v1)]
+            sch.append(("c", i))
+            t0, v0 = t1, v1
+        sch += [("v", k) for k in range(v0, c.v_num_hidden_layers)]
+        sch += [("t", k) for k in range(t0, c.num_hidden_layers)]
+        return sch
+
+    # ------------------------------------------------------------ forward
+    def forward(self, batch, train=True, noise=None, ent_neg=None, val_neg=None, seed=None):
+        """Runs the forward of the step; returns (losses dict of device tensors, ctx for backward).
+
+        batch: dict of device tensors with the reference names (A0 in SURVEY.md §8(a)).
+        noise: optional {v,t,pv: [B, L, 3, D]} gumbel noise; ent_neg/val_neg optional [B,NPV,2]."""
+        c = self.cfg
+        fp = self.fp
+        dev = self.device
+        H, Hv = self.H, self.Hv
+        ids, tt, mt = batch["input_ids"], batch["segment_ids"], batch["input_mask"]
+        pids, ptt, mp = batch["input_ids_pv"], batch["segment_ids_pv"], batch["input_mask_pv"]
+        feat, loc, mv = batch["image_feat"], batch["image_loc"], batch["image_mask"]
+        B, T = ids.shape
+        P = pids.shape[1]
+        R = feat.shape[1]
+        BT, BP, BR = B * T, B * P, B * R
+        rng = Rng(self.base_seed * 1000003 + (seed if seed is not None else self.step_count))
+        ph = self.p_h if train else 0.0
+        pvh = self.p_vh if train else 0.0
+        ctx = {"B": B, "T": T, "P": P, "R": R, "train": train, "seed": rng.seed}
+
+        mask_t, mask_p, mask_v = _ext_mask(mt), _ext_mask(mp), _ext_mask(mv)
+        mask_t2 = torch.cat([mask_t, mask_t]).contiguous()
+        mask_p2 = torch.cat([mask_p, mask_p]).contiguous()
+        mask_v2 = torch.cat([mask_v, mask_v]).contiguous()
+
+        # ---- embeddings (BertEmbeddings x2, BertImageEmbeddings)
+        Nt = 2 * BT + 2 * BP
+        XT = torch.empty((Nt, H), dtype=torch.float32, device=dev)
+        ind_t = torch.empty((BT, H), dtype=torch.float32, device=dev)
+        ind_pv = torch.empty((BP, H), dtype=torch.float32, device=dev)
+        xh_t = torch.empty_like(ind_t)
+        rs_t = torch.empty((BT,), dtype=torch.float32, device=dev)
+        xh_p = torch.empty_like(ind_pv)
+        rs_p = torch.empty((BP,), dtype=torch.float32, device=dev)
+        off_t = rng.take(BT * H) if ph > 0 else 0
+        ops.embed_fwd(ids, tt, fp.p["embeddings.word_embeddings.weight"], fp.p["embeddings.position_embeddings.weight"],
+                      fp.p["embeddings.token_type_embeddings.weight"], self.emb_ln.g, self.emb_ln.b, ind_t, XT[0:BT],
+                      XT[BT:2 * BT], xh_t, rs_t, ph, rng.seed, off_t)
+        off_p = rng.take(BP * H) if ph > 0 else 0
+        ops.embed_fwd(pids, ptt, fp.p["embeddings.word_embeddings.weight"], fp.p["embeddings.position_embeddings.weight"],
+                      fp.p["embeddings.token_type_embeddings.weight"], self.emb_ln.g, self.emb_ln.b, ind_pv,
+                      XT[2 * BT:2 * BT + BP], XT[2 * BT + BP:], xh_p, rs_p, ph, rng.seed, off_p)
+        ctx["emb"] = (xh_t, rs_t, off_t, xh_p, rs_p, off_p)
+
+        feat2 = feat.reshape(BR, feat.shape[2])
+        loc2 = loc.reshape(BR, loc.shape[2])
+        img = self.vemb_img.fwd(feat2)
+        lce = self.vemb_loc.fwd(loc2)
+        ind_v = torch.empty((BR, Hv), dtype=torch.float32, device=dev)
+        xh_v = torch.empty_like(ind_v)
+        rs_v = torch.empty((BR,), dtype=torch.float32, device=dev)
+        off_v = rng.take(BR * Hv) if ph > 0 else 0
+        ops.ln_fwd(img, lce, self.vemb_ln.g, self.vemb_ln.b, ind_v, xh_v, rs_v, p_out=ph, seed=rng.seed, off_out=off_v)
+        XV = torch.empty((2 * BR, Hv), dtype=torch.float32, device=dev)
+        XV[0:BR].copy_(ind_v)
+        XV[BR:].copy_(ind_v)
+        ctx["vemb"] = (feat2, loc2, xh_v, rs_v, off_v)
+
+        # ---- encoder, lock-step wide passes
+        tsegs = [(0, 2 * B, T, mask_t2), (2 * BT, 2 * B, P, mask_p2)]
+        vsegs = [(0, 2 * B, R, mask_v2)]
+        enc = []
+        for kind, i in self.schedule:
+            if kind == "t":
+                op = self.text[i]
+                if not train:
+                    op = _eval_view(op)
+                XT, sv = op.fwd(XT, tsegs, rng)
+                enc.append((kind, i, sv))
+            elif kind == "v":
+                op = self.image[i]
+                if not train:
+                    op = _eval_view(op)
+                XV, sv = op.fwd(XV, vsegs, rng)
+                enc.append((kind, i, sv))
+            else:
+                XT2 = torch.empty_like(XT)
+                XV2 = torch.empty_like(XV)
+                ops_ = [self.co_tv[i], self.co_pv[i], self.co_tt[i]]
+                if not train:
+                    ops_ = [_eval_view(o) for o in ops_]
+                s_tv = ops_[0].fwd(XV[0:BR], XT[0:BT], B, R, T, mask_v, mask_t, rng, XV2[0:BR], XT2[0:BT])
+                s_pv = ops_[1].fwd(XV[BR:], XT[2 * BT:2 * BT + BP], B, R, P, mask_v, mask_p, rng, XV2[BR:],
+                                   XT2[2 * BT:2 * BT + BP])
+                s_tt = ops_[2].fwd(XT[2 * BT + BP:], XT[BT:2 * BT], B, P, T, mask_p, mask_t, rng,
+                                   XT2[2 * BT + BP:], XT2[BT:2 * BT])
+                enc.append((kind, i, (s_tv, s_pv, s_tt, ops_)))
+                XT, XV = XT2, XV2
+        ctx["enc"] = enc
+        ctx["XT"], ctx["XV"] = XT, XV
+
+        # ---- initial-interactive fusion (get_sequence_pooled_output_final :2376-2411)
+        mode = getattr(c, "if_pre_sampling", 1)
+        seq_tp = torch.empty((BT + BP, H), dtype=torch.float32, device=dev)
+        seq_v = torch.empty((BR, Hv), dtype=torch.float32, device=dev)
+        streams = {
+            "v": (ind_v, XV[0:BR], XV[BR:], seq_v, Hv),
+            "t": (ind_t, XT[0:BT], XT[BT:2 * BT], seq_tp[0:BT], H),
+            "pv": (ind_pv, XT[2 * BT:2 * BT + BP], XT[2 * BT + BP:], seq_tp[BT:], H),
+        }
+        fus = {}
+        for m in ("v", "t", "pv"):
+            x0, x1, x2, out, D = streams[m]
+            rows = x0.shape[0]
+            if mode == 1:
+                cc = torch.empty((rows, 3 * D), dtype=torch.float32, device=dev)
+                L.call("k3m_relu_cat3", x0.data_ptr(), x1.data_ptr(), x2.data_ptr(), cc.data_ptr(), rows, D, L.F32,
+                       L.stream())
+                a = self.gate[m].fwd(cc, epi=L.EPI_BIAS_SIGMOID)
+                ys = torch.empty_like(a)
+                idx = torch.empty((rows * D,), dtype=torch.uint8, device=dev)
+                nz = None
+                off_g = 0
+                if noise is not None:
+                    nz = noise[m].reshape(rows * 3 * D).to(device=dev, dtype=torch.float32).contiguous()
+                else:
+                    off_g = rng.take(rows * 3 * D)
+                L.call("k3m_gate_fwd", a.data_ptr(), cc.data_ptr(), L.ptr(nz), ys.data_ptr(), idx.data_ptr(),
+                       out.data_ptr(), rows, D, rng.seed, off_g, L.F32, L.stream())
+                fus[m] = (cc, a, ys, idx)
+            elif mode == 0:
+                L.call("k3m_mean3", x0.data_ptr(), x1.data_ptr(), x2.data_ptr(), out.data_ptr(), out.numel(), L.F32,
+                       L.stream())
+                fus[m] = None
+            else:
+                raise NotImplementedError("if_pre_sampling=%s" % mode)
+        ctx["fus"] = (fus, streams, mode)
+        ctx["seq_tp"], ctx["seq_v"] = seq_tp, seq_v
+
+        # ---- pooled outputs and c_initial (:2404-2409, :2722-2725)
+        mean_v = torch.empty((B, Hv), dtype=torch.float32, device=dev)
+        pooled_t = torch.empty((B, H), dtype=torch.float32, device=dev)
+        pooled_pv = torch.empty((B, H), dtype=torch.float32, device=dev)
+        L.call("k3m_seq_mean", seq_v.data_ptr(), B, R, 1, Hv, 1.0, mean_v.data_ptr(), 0, L.F32, L.stream())
+        L.call("k3m_seq_mean", seq_tp.data_ptr(), B, T, 1, H, 1.0, pooled_t.data_ptr(), 0, L.F32, L.stream())
+        L.call("k3m_seq_mean", seq_tp[BT:].data_ptr(), B, P, 1, H, 1.0, pooled_pv.data_ptr(), 0, L.F32, L.stream())
+        pooled_v = self.map_b2i.fwd(mean_v)
+        c_init = torch.empty((B, H), dtype=torch.float32, device=dev)
+        L.call("k3m_mean3", pooled_v.data_ptr(), pooled_t.data_ptr(), pooled_pv.data_ptr(), c_init.data_ptr(),
+               c_init.numel(), L.F32, L.stream())
+        ctx["pool"] = (mean_v,)
+
+        # ---- structure aggregator + LPM (:2413-2505)
+        index_p, index_v = batch["index_p"].contiguous(), batch["index_v"].contiguous()
+        NPV = index_p.shape[1]
+        X = torch.empty((B * NPV, 3 * H), dtype=torch.float32, device=dev)
+        nvalid = torch.empty((B,), dtype=torch.int32, device=dev)
+        src = torch.empty((B,), dtype=torch.int32, device=dev)
+        L.call("k3m_sa_gather", seq_tp[BT:].data_ptr(), index_p.data_ptr(), index_v.data_ptr(), c_init.data_ptr(),
+               X.data_ptr(), nvalid.data_ptr(), src.data_ptr(), B, P, NPV, H, L.F32, L.stream())
+        Tm = self.sw1.fwd(X)
+        att = torch.empty((B, NPV), dtype=torch.float32, device=dev)
+        agg = torch.empty((B, H), dtype=torch.float32, device=dev)
+        L.call("k3m_sa_attn_fwd", Tm.data_ptr(), nvalid.data_ptr(), src.data_ptr(), fp.p["struc_w2.weight"].data_ptr(),
+               fp.p["struc_w2.bias"].data_ptr(), c_init.data_ptr(), att.data_ptr(), agg.data_ptr(), B, NPV, H,
+               L.stream())
+        c_final = c_init.clone()
+        self.sw3.fwd(agg, out=c_final, beta=1.0)
+        if ent_neg is None:
+            ent_neg = torch.empty((B, NPV, 2), dtype=torch.int64, device=dev)
+            val_neg = torch.empty((B, NPV, 2), dtype=torch.int64, device=dev)
+            nneg = getattr(c, "num_negative_pv", 4)
+            L.call("k3m_lpm_sample", nvalid.data_ptr(), B, NPV, nneg // 2, nneg - nneg // 2, rng.seed,
+                   rng.take(B * NPV * 4), ent_neg.data_ptr(), val_neg.data_ptr(), L.stream())
+        else:
+            ent_neg = ent_neg.to(device=dev, dtype=torch.int64).contiguous()
+            val_neg = val_neg.to(device=dev, dtype=torch.int64).contiguous()
+        lpm = torch.empty((1,), dtype=torch.float32, device=dev)
+        lws = torch.empty((B * NPV * 9 + 2,), dtype=torch.float32, device=dev)
+        margin = float(getattr(c, "margin", 1.0))
+        L.call("k3m_lpm_fwd", c_final.data_ptr(), X.data_ptr(), nvalid.data_ptr(), ent_neg.data_ptr(),
+               val_neg.data_ptr(), B, NPV, H, margin, lpm.data_ptr(), lws.data_ptr(), L.stream())
+        ctx["struct"] = (X, nvalid, src, Tm, att, agg, c_init, c_final, ent_neg, val_neg, lws, index_p, index_v, NPV,
+                         margin)
+
+        # ---- heads on labelled rows only (unlabelled logits do not reach the loss or the gradients)
+        losses = torch.zeros((4,), dtype=torch.float32, device=dev)   # mlm_t, mlm_pv, img, -
+        nmax = BT + BP
+        idx_m = torch.empty((nmax,), dtype=torch.int32, device=dev)
+        lab_m = torch.empty((nmax,), dtype=torch.int64, device=dev)
+        sc_m = torch.empty((nmax,), dtype=torch.float32, device=dev)
+        sl_m = torch.empty((nmax,), dtype=torch.int32, device=dev)
+        cnt = torch.zeros((2,), dtype=torch.int32, device=dev)
+        L.call("k3m_compact_labels_ex", batch["lm_label_ids"].contiguous().data_ptr(), BT, 0, T, T, 0, 0,
+               idx_m.data_ptr(), lab_m.data_ptr(), None, sc_m.data_ptr(), sl_m.data_ptr(), cnt.data_ptr(), L.stream())
+        L.call("k3m_compact_labels_ex", batch["lm_label_ids_pv"].contiguous().data_ptr(), BP, 0, P, P, BT, 1,
+               idx_m.data_ptr(), lab_m.data_ptr(), None, sc_m.data_ptr(), sl_m.data_ptr(), cnt.data_ptr(), L.stream())
+        R1 = R - 1
+        idx_v = torch.empty((B * R1,), dtype=torch.int32, device=dev)
+        src_v = torch.empty((B * R1,), dtype=torch.int32, device=dev)
+        sc_v = torch.empty((B * R1,), dtype=torch.float32, device=dev)
+        sl_v = torch.empty((B * R1,), dtype=torch.int32, device=dev)
+        cnt_v = cnt[1:2]
+        L.call("k3m_compact_labels_ex", batch["image_label"].contiguous().data_ptr(), B * R1, 1, R1, R, 1, 2,
+               idx_v.data_ptr(), None, src_v.data_ptr(), sc_v.data_ptr(), sl_v.data_ptr(), cnt_v.data_ptr(),
+               L.stream())
+        n_m, n_v = [int(x) for x in cnt.tolist()]   # one host sync per step (labelled-row counts)
+
+        V = c.vocab_size
+        hm = torch.empty((n_m, H), dtype=torch.float32, device=dev)
+        ops.gather_rows(seq_tp, idx_m, n_m, hm)
+        pre_m = torch.empty_like(hm)
+        hm1 = self.mlm_t.fwd(hm, epi=L.EPI_BIAS_GELU, aux=pre_m)
+        hl = torch.empty_like(hm)
+        xh_m = torch.empty_like(hm)
+        rs_m = torch.empty((n_m,), dtype=torch.float32, device=dev)
+        if n_m:
+            ops.ln_fwd(hm1, None, self.mlm_ln.g, self.mlm_ln.b, hl, xh_m, rs_m)
+        E = fp.p["embeddings.word_embeddings.weight"]
+        logits = ops.linear(hl, E, fp.p["cls.predictions.bias"])
+        lr_m = torch.empty((n_m,), dtype=torch.float32, device=dev)
+        L.call("k3m_ce_fwd_bwd", logits.data_ptr(), V, lab_m.data_ptr(), sc_m.data_ptr(), n_m, V, lr_m.data_ptr(),
+               L.stream())
+        if n_m:
+            L.call("k3m_loss_reduce", lr_m.data_ptr(), sc_m.data_ptr(), sl_m.data_ptr(), n_m, losses.data_ptr(),
+                   L.stream())
+        ctx["mlm"] = (idx_m, n_m, hm, pre_m, hl, xh_m, rs_m, logits)
+
+        Cv = c.v_target_size
+        hv = torch.empty((n_v, Hv), dtype=torch.float32, device=dev)
+        ops.gather_rows(seq_v, idx_v, n_v, hv)
+        pre_v = torch.empty_like(hv)
+        hv1 = self.img_t.fwd(hv, epi=L.EPI_BIAS_GELU, aux=pre_v)
+        hlv = torch.empty_like(hv)
+        xh_iv = torch.empty_like(hv)
+        rs_iv = torch.empty((n_v,), dtype=torch.float32, device=dev)
+        if n_v:
+            ops.ln_fwd(hv1, None, self.img_ln.g, self.img_ln.b, hlv, xh_iv, rs_iv)
+        lv = self.img_dec.fwd(hlv)
+        tgt = batch["image_target"].reshape(B * R1, Cv).contiguous()
+        lr_v = torch.empty((n_v,), dtype=torch.float32, device=dev)
+        L.call("k3m_kl_fwd_bwd", lv.data_ptr(), Cv, tgt.data_ptr(), Cv, src_v.data_ptr(), sc_v.data_ptr(), n_v, Cv,
+               lr_v.data_ptr(), L.stream())
+        if n_v:
+            L.call("k3m_loss_reduce", lr_v.data_ptr(), sc_v.data_ptr(), sl_v.data_ptr(), n_v, losses.data_ptr(),
+                   L.stream())
+        else:
+            losses[2] = float("nan")   # 0/0 as in the reference (:2758-2760)
+        ctx["img"] = (idx_v, n_v, hv, pre_v, hlv, xh_iv, rs_iv, lv)
+
+        nsp = torch.empty((1,), dtype=torch.float32, device=dev)
+        L.call("k3m_nsp_loss", pooled_t.data_ptr(), pooled_pv.data_ptr(), pooled_v.data_ptr(),
+               fp.p["cls.seq_relationship.weight"].data_ptr(), fp.p["cls.seq_relationship.bias"].data_ptr(),
+               batch["is_next"].contiguous().data_ptr(), batch["is_next_pv_v"].contiguous().data_ptr(),
+               batch["is_next_pv_t"].contiguous().data_ptr(), B, H, nsp.data_ptr(), L.stream())
+        out = {
+            "masked_lm_loss": losses[0:1], "masked_lm_loss_pv": losses[1:2], "masked_img_loss": losses[2:3],
+            "loss_lpm": lpm, "next_sentence_loss": nsp, "c_initial": c_init, "c_final": c_final,
+            "pooled_t": pooled_t, "pooled_pv": pooled_pv, "pooled_v": pooled_v,
+        }
+        out["loss"] = losses[0:1] + losses[1:2] + losses[2:3] + lpm
+        ctx["batch"] = batch
+        return out, ctx
+
+    # ------------------------------------------------------------ backward
+    def backward(self, ctx, w_mlm=1.0, w_img=1.0, w_lpm=1.0, grad_ready=None):
+        """Backward of  w_mlm*(mlm_t + mlm_pv) + w_img*img + w_lpm*lpm  (train_concap_struc.py:533).
+        Parameter gradients are ACCUMULATED into self.fp.grad.  grad_ready(kind, index) is called as
+        soon as the gradients of an encoder block are final (DDP bucket hook)."""
+        c = self.cfg
+        fp = self.fp
+        dev = self.device
+        H, Hv = self.H, self.Hv
+        B, T, P, R = ctx["B"], ctx["T"], ctx["P"], ctx["R"]
+        BT, BP, BR = B * T, B * P, B * R
+        batch = ctx["batch"]
+        seq_tp, seq_v = ctx["seq_tp"], ctx["seq_v"]
+        dseq_tp = torch.zeros_like(seq_tp)
+        dseq_v = torch.zeros_like(seq_v)
+
+        # ---- MLM head (dlogits already in place from the forward CE kernel)
+        idx_m, n_m, hm, pre_m, hl, xh_m, rs_m, dlog = ctx["mlm"]
+        if n_m:
+            E = fp.p["embeddings.word_embeddings.weight"]
+            gE = fp.g["embeddings.word_embeddings.weight"]
+            dhl = ops.linear_dgrad(dlog, E, alpha=w_mlm)
+            ops.linear_wgrad(dlog, hl, gE, fp.g["cls.predictions.bias"], alpha=w_mlm)
+            dh1 = torch.empty_like(hl)
+            ops.ln_bwd(dhl, xh_m, rs_m, self.mlm_ln.g, dh1, dh1, self.mlm_ln.gg, self.mlm_ln.gb)
+            du = torch.empty_like(hl)
+            ops.dgelu(dh1, pre_m, du)
+            self.mlm_t.wgrad(du, hm)
+            dhm = self.mlm_t.dgrad(du)
+            ops.scatter_add_rows(dhm, idx_m, n_m, dseq_tp)
+        idx_v, n_v, hv, pre_v, hlv, xh_iv, rs_iv, dlv = ctx["img"]
+        if n_v:
+            dhlv = self.img_dec.dgrad(dlv, alpha=w_img)
+            self.img_dec.wgrad(dlv, hlv, alpha=w_img)
+            dh1v = torch.empty_like(hlv)
+            ops.ln_bwd(dhlv, xh_iv, rs_iv, self.img_ln.g, dh1v, dh1v, self.img_ln.gg, self.img_ln.gb)
+            duv = torch.empty_like(hlv)
+            ops.dgelu(dh1v, pre_v, duv)
+            self.img_t.wgrad(duv, hv)
+            dhv = self.img_t.dgrad(duv)
+            ops.scatter_add_rows(dhv, idx_v, n_v, dseq_v)
+
+        # ---- structure aggregator + LPM
+        (X, nvalid, src, Tm, att, agg, c_init, c_final, ent_neg, val_neg, lws, index_p, index_v, NPV,
+         margin) = ctx["struct"]
+        dcf = torch.zeros_like(c_final)
+        dX = torch.zeros_like(X)
+        L.call("k3m_lpm_bwd", c_final.data_ptr(), X.data_ptr(), nvalid.data_ptr(), ent_neg.data_ptr(),
+               val_neg.data_ptr(), B, NPV, H, margin, lws.data_ptr(), dcf.data_ptr(), dX.data_ptr(), L.stream())
+        if w_lpm != 1.0:
+            ops.add_(dcf, dcf.clone(), w_lpm - 1.0)
+            ops.add_(dX, dX.clone(), w_lpm - 1.0)
+        if "d_c_final" in ctx:
+            ops.add_(dcf, ctx["d_c_final"].contiguous())
+        dagg = self.sw3.dgrad(dcf)
+        self.sw3.wgrad(dcf, agg)
+        dci = dcf.clone()                                   # c_final = c_init + ...
+        if "d_c_initial" in ctx:
+            ops.add_(dci, ctx["d_c_initial"].contiguous())
+        dT = torch.zeros_like(Tm)
+        L.call("k3m_sa_attn_bwd", dagg.data_ptr(), Tm.data_ptr(), att.data_ptr(), nvalid.data_ptr(), src.data_ptr(),
+               fp.p["struc_w2.weight"].data_ptr(), dT.data_ptr(), fp.g["struc_w2.weight"].data_ptr(),
+               fp.g["struc_w2.bias"].data_ptr(), dci.data_ptr(), B, NPV, H, L.stream())
+        self.sw1.wgrad(dT, X)
+        self.sw1.dgrad(dT, dx=dX, beta=1.0)
+        L.call("k3m_sa_gather_bwd", dX.data_ptr(), index_p.data_ptr(), index_v.data_ptr(), nvalid.data_ptr(),
+               dseq_tp[BT:].data_ptr(), dci.data_ptr(), B, P, NPV, H, L.F32, L.stream())
+
+        # ---- pooled outputs
+        (mean_v,) = ctx["pool"]
+        dpv = torch.empty((B, H), dtype=torch.float32, device=dev)
+        dpt = torch.empty_like(dpv)
+        dppv = torch.empty_like(dpv)
+        L.call("k3m_mean3_bwd", dci.data_ptr(), dpv.data_ptr(), dpt.data_ptr(), dppv.data_ptr(), dci.numel(), 0, L.F32,
+               L.stream())
+        dmean_v = self.map_b2i.dgrad(dpv)
+        self.map_b2i.wgrad(dpv, mean_v)
+        L.call("k3m_seq_mean_bwd", dmean_v.data_ptr(), B, R, 1, Hv, 1.0, dseq_v.data_ptr(), L.F32, L.stream())
+        L.call("k3m_seq_mean_bwd", dpt.data_ptr(), B, T, 1, H, 1.0, dseq_tp.data_ptr(), L.F32, L.stream())
+        L.call("k3m_seq_mean_bwd", dppv.data_ptr(), B, P, 1, H, 1.0, dseq_tp[BT:].data_ptr(), L.F32, L.stream())
+
+        # ---- fusion
+        fus, streams, mode = ctx["fus"]
+        XT, XV = ctx["XT"], ctx["XV"]
+        dXT = torch.empty_like(XT)
+        dXV = torch.empty_like(XV)
+        d_ind = {}
+        dslices = {
+            "v": (dXV[0:BR], dXV[BR:], dseq_v),
+            "t": (dXT[0:BT], dXT[BT:2 * BT], dseq_tp[0:BT]),
+            "pv": (dXT[2 * BT:2 * BT + BP], dXT[2 * BT + BP:], dseq_tp[BT:]),
+        }
+        for m in ("v", "t", "pv"):
+            x0 = streams[m][0]
+            D = streams[m][4]
+            rows = x0.shape[0]
+            d1, d2, dout = dslices[m]
+            d0 = torch.empty_like(x0)
+            if mode == 1:
+                cc, a, ys, idx = fus[m]
+                dc = torch.empty_like(cc)
+                dpre = torch.empty_like(cc)
+                L.call("k3m_gate_bwd", dout.data_ptr(), a.data_ptr(), cc.data_ptr(), ys.data_ptr(), idx.data_ptr(),
+                       dc.data_ptr(), dpre.data_ptr(), rows, D, L.F32, L.stream())
+                self.gate[m].dgrad(dpre, dx=dc, beta=1.0)
+                self.gate[m].wgrad(dpre, cc)
+                L.call("k3m_relu_split3_bwd", dc.data_ptr(), cc.data_ptr(), d0.data_ptr(), d1.data_ptr(), d2.data_ptr(),
+                       rows, D, 0, L.F32, L.stream())
+            else:
+                L.call("k3m_mean3_bwd", dout.data_ptr(), d0.data_ptr(), d1.data_ptr(), d2.data_ptr(), dout.numel(), 0,
+                       L.F32, L.stream())
+            d_ind[m] = d0
+
+        # ---- encoder (reverse lock-step)
+        for kind, i, sv in reversed(ctx["enc"]):
+            if kind == "t":
+                op = self.text[i] if ctx["train"] else _eval_view(self.text[i])
+                dXT = op.bwd(dXT, sv)
+            elif kind == "v":
+                op = self.image[i] if ctx["train"] else _eval_view(self.image[i])
+                dXV = op.bwd(dXV, sv)
+            else:
+                s_tv, s_pv, s_tt, ops_ = sv
+                dXT2 = torch.empty_like(dXT)
+                dXV2 = torch.empty_like(dXV)
+                ops_[0].bwd(dXV[0:BR], dXT[0:BT], s_tv, dXV2[0:BR], dXT2[0:BT])
+                ops_[1].bwd(dXV[BR:], dXT[2 * BT:2 * BT + BP], s_pv, dXV2[BR:], dXT2[2 * BT:2 * BT + BP])
+                ops_[2].bwd(dXT[2 * BT + BP:], dXT[BT:2 * BT], s_tt, dXT2[2 * BT + BP:], dXT2[BT:2 * BT])
+                dXT, dXV = dXT2, dXV2
+            if grad_ready is not None:
+                grad_ready(kind, i)
+
+        # ---- embeddings
+        ph = self.p_h if ctx["train"] else 0.0
+        dt_ = d_ind["t"]
+        ops.add_(dt_, dXT[0:BT].contiguous())
+        ops.add_(dt_, dXT[BT:2 * BT].contiguous())
+        dp_ = d_ind["pv"]
+        ops.add_(dp_, dXT[2 * BT:2 * BT + BP].contiguous())
+        ops.add_(dp_, dXT[2 * BT + BP:].contiguous())
+        dv_ = d_ind["v"]
+        ops.add_(dv_, dXV[0:BR].contiguous())
+        ops.add_(dv_, dXV[BR:].contiguous())
+        xh_t, rs_t, off_t, xh_p, rs_p, off_p = ctx["emb"]
+        gword = fp.g["embeddings.word_embeddings.weight"]
+        gpos = fp.g["embeddings.position_embeddings.weight"]
+        gtyp = fp.g["embeddings.token_type_embeddings.weight"]
+        for dy, xh, rs, off, ids, tt in ((dt_, xh_t, rs_t, off_t, batch["input_ids"], batch["segment_ids"]),
+                                         (dp_, xh_p, rs_p, off_p, batch["input_ids_pv"], batch["segment_ids_pv"])):
+            ds = torch.empty_like(dy)
+            ops.ln_bwd(dy, xh, rs, self.emb_ln.g, ds, ds, self.emb_ln.gg, self.emb_ln.gb, p_out=ph,
+                       seed=ctx["seed"], off_out=off)
+            ops.embed_bwd(ids.contiguous(), tt.contiguous(), ds, gword, gpos, gtyp)
+        feat2, loc2, xh_v, rs_v, off_v = ctx["vemb"]
+        dsv = torch.empty_like(dv_)
+        ops.ln_bwd(dv_, xh_v, rs_v, self.vemb_ln.g, dsv, dsv, self.vemb_ln.gg, self.vemb_ln.gb, p_out=ph,
+                   seed=ctx["seed"], off_out=off_v)
+        self.vemb_img.wgrad(dsv, feat2)
+        self.vemb_loc.wgrad(dsv, loc2)
+        if grad_ready is not None:
+            grad_ready("emb", 0)
+
+
+def _eval_view(op):
+    """Same op with every dropout probability set to zero (model.eval())."""
+    import copy
+    o = copy.copy(op)
+    for k, v in list(vars(o).items()):
+        if isinstance(v, AddLN):
+            setattr(o, k, AddLN(v.ln, 0.0))
+        elif isinstance(v, FFN):
+            f = copy.copy(v)
+            f.tail = AddLN(v.tail.ln, 0.0)
+            setattr(o, k, f)
+        elif k in ("p_attn", "pa1", "pa2"):
+            setattr(o, k, 0.0)
+    return o

@@ -1,0 +1,152 @@
+"""Tensor-level wrappers over the C ABI (k3m_amd/_lib.py).  Every function launches libk3m_hip
+kernels on torch's current stream; torch is used only to allocate outputs/workspaces."""
+import torch
+
+from . import _lib as L
+from ._lib import call, ptr, stream
+
+_DT = {torch.float32: L.F32, torch.bfloat16: L.BF16}
+
+
+def dt(t):
+    return _DT[t.dtype]
+
+
+def _ld(t):
+    assert t.dim() == 2 and t.stride(1) == 1, "row-major 2-D view expected"
+    return t.stride(0)
+
+
+def empty(shape, like=None, dtype=torch.float32, device=None):
+    return torch.empty(shape, dtype=dtype, device=device if device is not None else like.device)
+
+
+# ------------------------------------------------------------------ GEMM
+def gemm(a, a_trans, b, b_trans, c, m, n, k, epi=L.EPI_NONE, bias=None, aux=None, alpha=1.0, beta=0.0, splitk=1,
+         ws=None):
+    g = L.K3mGemm()
+    g.m, g.n, g.k = m, n, k
+    g.a_trans, g.b_trans = a_trans, b_trans
+    g.epilogue, g.dtype, g.splitk = epi, dt(c), splitk
+    g.lda, g.ldb, g.ldc = _ld(a), _ld(b), _ld(c)
+    g.ldaux = _ld(aux) if aux is not None else 0
+    g.a, g.b, g.c = ptr(a), ptr(b), ptr(c)
+    g.bias, g.aux, g.ws = ptr(bias), ptr(aux), ptr(ws)
+    g.alpha, g.beta = alpha, beta
+    call("k3m_gemm", L.C.byref(g), stream())
+    return c
+
+
+def linear(x, W, b=None, out=None, epi=None, aux=None, alpha=1.0, beta=0.0):
+    """out = x . W^T (+ b) with epilogue; x [M,K] (row view), W [N,K]."""
+    M, K = x.shape
+    N = W.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    if epi is None:
+        epi = L.EPI_BIAS if b is not None else L.EPI_NONE
+    return gemm(x, 0, W, 1, out, M, N, K, epi, b, aux, alpha, beta)
+
+
+def linear_dgrad(dy, W, dx=None, beta=0.0, dgelu_aux=None, alpha=1.0):
+    """dx (+)= dy . W (optionally * gelu'(aux)); dy [M,N], W [N,K]."""
+    M, N = dy.shape
+    K = W.shape[1]
+    if dx is None:
+        dx = torch.empty((M, K), dtype=dy.dtype, device=dy.device)
+    epi = L.EPI_DGELU if dgelu_aux is not None else L.EPI_NONE
+    return gemm(dy, 0, W, 0, dx, M, K, N, epi, None, dgelu_aux, alpha, beta)
+
+
+def _splitk(m, n, k):
+    tiles = ((m + 127) // 128) * ((n + 127) // 128)
+    if tiles >= 384 or k < 1024:
+        return 1
+    s = min(max(1, 768 // tiles), k // 512, 32)
+    return max(1, s)
+
+
+def linear_wgrad(dy, x, gW, gb=None, alpha=1.0):
+    """gW += alpha * dy^T . x ; gb += alpha * colsum(dy).  dy [M,N], x [M,K], gW [N,K] fp32."""
+    M, N = dy.shape
+    K = x.shape[1]
+    s = _splitk(N, K, M)
+    ws = torch.empty((s * N * K,), dtype=torch.float32, device=dy.device) if s > 1 else None
+    gemm(dy, 1, x, 0, gW, N, K, M, L.EPI_NONE, None, None, alpha, 1.0, s, ws)
+    if gb is not None:
+        colsum(dy, gb, accumulate=True, alpha=alpha)
+
+
+def colsum(x, out, accumulate=True, alpha=1.0):
+    rows, cols = x.shape
+    ws = torch.empty((64 * cols,), dtype=torch.float32, device=x.device)
+    if alpha == 1.0:
+        call("k3m_colsum", ptr(x), _ld(x), rows, cols, ptr(out), int(accumulate), ptr(ws), dt(x), stream())
+    else:
+        tmp = torch.empty((cols,), dtype=torch.float32, device=x.device)
+        call("k3m_colsum", ptr(x), _ld(x), rows, cols, ptr(tmp), 0, ptr(ws), dt(x), stream())
+        if accumulate:
+            add_(out, tmp, alpha)
+        else:
+            out.zero_()
+            add_(out, tmp, alpha)
+
+
+# ------------------------------------------------------------------ LayerNorm / embeddings
+def ln_fwd(x, res, gamma, beta, y, xhat, rstd, p_in=0.0, p_out=0.0, seed=0, off_in=0, off_out=0, eps=1e-12):
+    rows, cols = x.shape
+    for t in (x, res, y, xhat):
+        assert t is None or (t.is_contiguous() or t.stride(0) == cols)
+    call("k3m_ln_fwd", ptr(x), ptr(res), ptr(gamma), ptr(beta), ptr(y), ptr(xhat), ptr(rstd), rows, cols, eps, p_in,
+         p_out, seed, off_in, off_out, dt(x), stream())
+
+
+def ln_bwd(dy, xhat, rstd, gamma, dres, dx, dgamma, dbeta, p_in=0.0, p_out=0.0, seed=0, off_in=0, off_out=0,
+           acc_res=False):
+    rows, cols = dy.shape
+    ws = torch.empty((2 * 128 * cols,), dtype=torch.float32, device=dy.device)
+    call("k3m_ln_bwd", ptr(dy), ptr(xhat), ptr(rstd), ptr(gamma), ptr(dres), ptr(dx), ptr(dgamma), ptr(dbeta), rows,
+         cols, p_in, p_out, seed, off_in, off_out, int(acc_res), ptr(ws), dt(dy), stream())
+
+
+def embed_fwd(ids, tt, word, pos, typ, gamma, beta, y0, y1, y2, xhat, rstd, p_out, seed, off, eps=1e-12):
+    nseq, ln = ids.shape
+    call("k3m_embed_fwd", ptr(ids), ptr(tt), ptr(word), ptr(pos), ptr(typ), ptr(gamma), ptr(beta), ptr(y0), ptr(y1),
+         ptr(y2), ptr(xhat), ptr(rstd), nseq, ln, word.shape[1], eps, p_out, seed, off, dt(y0), stream())
+
+
+def embed_bwd(ids, tt, ds, dword, dpos, dtyp):
+    nseq, ln = ids.shape
+    call("k3m_embed_bwd", ptr(ids), ptr(tt), ptr(ds), ptr(dword), ptr(dpos), ptr(dtyp), nseq, ln, dword.shape[1],
+         dt(ds), stream())
+
+
+# ------------------------------------------------------------------ attention
+def attn_fwd(q, k, v, kmask, ctx, probs, nseq, lq, lk, nh, hd, scale, p_drop, seed, off):
+    call("k3m_attn_fwd", ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v), ptr(kmask), ptr(ctx), _ld(ctx), ptr(probs),
+         nseq, lq, lk, nh, hd, scale, p_drop, seed, off, dt(ctx), stream())
+
+
+def attn_bwd(dctx, q, k, v, probs, dq, dk, dv, nseq, lq, lk, nh, hd, scale, p_drop, seed, off):
+    call("k3m_attn_bwd", ptr(dctx), _ld(dctx), ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v), ptr(probs), ptr(dq),
+         ptr(dk), ptr(dv), _ld(dq), _ld(dk), _ld(dv), nseq, lq, lk, nh, hd, scale, p_drop, seed, off, dt(dctx),
+         stream())
+
+
+# ------------------------------------------------------------------ elementwise / rows
+def dgelu(g, pre, out):
+    call("k3m_dgelu", ptr(g), ptr(pre), ptr(out), g.numel(), dt(g), stream())
+
+
+def add_(y, x, alpha=1.0):
+    assert y.is_contiguous() and x.is_contiguous() and y.numel() == x.numel()
+    call("k3m_add_inplace", ptr(y), ptr(x), y.numel(), alpha, dt(y), stream())
+
+
+def gather_rows(src, idx, n, out):
+    call("k3m_gather_rows", ptr(src), _ld(src), ptr(idx), n, src.shape[1], ptr(out), _ld(out), dt(src), stream())
+
+
+def scatter_add_rows(src, idx, n, dst):
+    call("k3m_scatter_add_rows", ptr(src), _ld(src), ptr(idx), n, src.shape[1], ptr(dst), _ld(dst), dt(src),
+         stream())

@@ -1,0 +1,29 @@
+#!/bin/bash
+# Run GPU steps in order; stop at the first step that faults / aborts / times out
+# (pytest exit 1 = test failures: keep going so later steps still report).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+step() {
+  local name=$1 limit=$2; shift 2
+  echo "== $name (limit ${limit}s): $*"
+  timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "stopping after $name (rc=$rc)"
+    exit $rc
+  fi
+}
+for s in "$@"; do
+  case $s in
+    kern) step kern 400 python -m pytest tests/test_gpu_kernels.py -q ;;
+    smoke) step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    parity) step parity 900 python -m pytest tests/test_gpu_parity.py -x -q ;;
+    gpu) step gputests 1200 python -m pytest tests -m gpu -q ;;
+    bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
+    benchq) step bench 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done

@@ -1,0 +1,28 @@
+"""The C-ABI library loads and exports every symbol include/k3m_hip.h declares (no GPU calls)."""
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared():
+    src = open(os.path.join(REPO, "include", "k3m_hip.h")).read()
+    return sorted(set(re.findall(r"^int (k3m_[a-z0-9_]+)\(", src, re.M)))
+
+
+def test_header_matches_binding_table():
+    from k3m_amd import _lib
+    assert declared() == sorted(_lib.SIGNATURES), "include/k3m_hip.h and k3m_amd/_lib.py disagree"
+
+
+def test_library_exports_every_symbol():
+    from k3m_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        from k3m_amd.build_lib import build
+        build()
+    got = _lib.exported_symbols()
+    assert sorted(got) == declared()
+    lib = _lib.load()
+    assert lib is not None

@@ -1,0 +1,231 @@
+"""Per-kernel numerics on the GPU against plain PyTorch fp32 references of the same op."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from k3m_amd import _lib
+    _lib.load()
+    return torch.device("cuda")
+
+
+def _rel(a, b):
+    return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+
+
+@pytest.mark.parametrize("m,n,k", [(128, 128, 64), (300, 200, 100), (2368, 1024, 2048), (37, 1601, 1024),
+                                   (64, 768, 5), (1000, 3072, 768)])
+@pytest.mark.parametrize("at,bt", [(0, 1), (0, 0), (1, 0), (1, 1)])
+def test_gemm_layouts(dev, m, n, k, at, bt):
+    from k3m_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(m * 7 + n + k)
+    A = torch.randn(m, k, generator=g).to(dev)
+    Bm = torch.randn(k, n, generator=g).to(dev)
+    a = A.t().contiguous() if at else A
+    b = Bm.t().contiguous() if bt else Bm
+    c = torch.randn(m, n, device=dev)
+    ref = 0.5 * (A @ Bm) + 0.25 * c
+    ops.gemm(a, at, b, bt, c, m, n, k, alpha=0.5, beta=0.25)
+    assert _rel(c, ref) < 1e-5
+
+
+@pytest.mark.parametrize("splitk", [2, 5])
+def test_gemm_splitk(dev, splitk):
+    from k3m_amd import ops
+    m, n, k = 768, 768, 20000
+    A = torch.randn(k, m, device=dev)
+    Bm = torch.randn(k, n, device=dev)
+    c = torch.randn(m, n, device=dev)
+    ref = A.t() @ Bm + c
+    ws = torch.empty(splitk * m * n, device=dev)
+    ops.gemm(A, 1, Bm, 0, c, m, n, k, beta=1.0, splitk=splitk, ws=ws)
+    assert _rel(c, ref) < 1e-5
+
+
+def test_gemm_epilogues(dev):
+    from k3m_amd import ops, _lib as L
+    x = torch.randn(500, 768, device=dev)
+    W = torch.randn(3072, 768, device=dev) * 0.05
+    b = torch.randn(3072, device=dev)
+    pre = torch.empty(500, 3072, device=dev)
+    y = ops.linear(x, W, b, epi=L.EPI_BIAS_GELU, aux=pre)
+    r = x @ W.t() + b
+    assert _rel(pre, r) < 1e-5
+    assert _rel(y, torch.nn.functional.gelu(r)) < 1e-5
+    s = ops.linear(x, W, b, epi=L.EPI_BIAS_SIGMOID)
+    assert _rel(s, torch.sigmoid(r)) < 1e-5
+    dy = torch.randn(500, 3072, device=dev)
+    W2 = torch.randn(3072, 768, device=dev) * 0.05
+    d = ops.linear_dgrad(dy, W2)
+    assert _rel(d, dy @ W2) < 1e-5
+    pre2 = torch.randn(500, 768, device=dev)
+    dx = ops.linear_dgrad(dy, W, dgelu_aux=pre2)
+    xr = pre2.clone().requires_grad_(True)
+    torch.nn.functional.gelu(xr).backward(dy @ W)
+    assert _rel(dx, xr.grad) < 1e-5
+
+
+def test_wgrad_colsum(dev):
+    from k3m_amd import ops
+    dy = torch.randn(20992, 768, device=dev)
+    x = torch.randn(20992, 3072, device=dev)
+    gW = torch.randn(768, 3072, device=dev)
+    gb = torch.randn(768, device=dev)
+    rW = gW + dy.t() @ x
+    rb = gb + dy.sum(0)
+    ops.linear_wgrad(dy, x, gW, gb)
+    assert _rel(gW, rW) < 1e-5
+    assert _rel(gb, rb) < 1e-5
+
+
+def _ln_ref(s, g, b):
+    u = s.mean(-1, keepdim=True)
+    v = (s - u).pow(2).mean(-1, keepdim=True)
+    return g * (s - u) / torch.sqrt(v + 1e-12) + b
+
+
+@pytest.mark.parametrize("cols", [768, 1024])
+def test_layernorm(dev, cols):
+    from k3m_amd import ops
+    M = 999
+    x = torch.randn(M, cols, device=dev)
+    r = torch.randn(M, cols, device=dev)
+    g = 1 + 0.1 * torch.randn(cols, device=dev)
+    b = 0.1 * torch.randn(cols, device=dev)
+    y = torch.empty_like(x)
+    xh = torch.empty_like(x)
+    rs = torch.empty(M, device=dev)
+    ops.ln_fwd(x, r, g, b, y, xh, rs)
+    xr, rr, gr, br = [t.clone().requires_grad_(True) for t in (x, r, g, b)]
+    yr = _ln_ref(xr + rr, gr, br)
+    assert _rel(y, yr) < 1e-5
+    dy = torch.randn_like(y)
+    yr.backward(dy)
+    dres = torch.empty_like(x)
+    dg = torch.zeros(cols, device=dev)
+    db = torch.zeros(cols, device=dev)
+    ops.ln_bwd(dy, xh, rs, g, dres, dres, dg, db)
+    assert _rel(dres, xr.grad) < 1e-4
+    assert _rel(dg, gr.grad) < 1e-4
+    assert _rel(db, br.grad) < 1e-4
+
+
+def test_dropout_ln_regenerates_mask(dev):
+    from k3m_amd import ops
+    M, cols = 512, 768
+    x = torch.randn(M, cols, device=dev)
+    g = torch.ones(cols, device=dev)
+    b = torch.zeros(cols, device=dev)
+    y, xh = torch.empty_like(x), torch.empty_like(x)
+    rs = torch.empty(M, device=dev)
+    ops.ln_fwd(x, None, g, b, y, xh, rs, p_in=0.1, seed=5, off_in=77)
+    dx, dres = torch.empty_like(x), torch.empty_like(x)
+    dg, db = torch.zeros(cols, device=dev), torch.zeros(cols, device=dev)
+    ops.ln_bwd(torch.randn_like(x), xh, rs, g, dres, dx, dg, db, p_in=0.1, seed=5, off_in=77)
+    frac = float((dx == 0).float().mean())
+    assert 0.08 < frac < 0.12
+    ratio = dx[dx != 0] / dres[dx != 0]
+    assert torch.allclose(ratio, torch.full_like(ratio, 1 / 0.9), rtol=1e-5)
+    # the forward used the same mask: dropped inputs did not reach the LN sum
+    s_ref = x.clone()
+    s_ref[dx == 0] = 0
+    s_ref = s_ref / 0.9 * (dx != 0) + 0 * s_ref
+    assert _rel(y, _ln_ref(s_ref, g, b)) < 1e-4
+
+
+def _attn_ref(q, k, v, mask, nh):
+    B, Lq, D = q.shape
+    Lk = k.shape[1]
+    hd = D // nh
+    qh = q.view(B, Lq, nh, hd).permute(0, 2, 1, 3)
+    kh = k.view(B, Lk, nh, hd).permute(0, 2, 1, 3)
+    vh = v.view(B, Lk, nh, hd).permute(0, 2, 1, 3)
+    s = qh @ kh.transpose(-1, -2) / math.sqrt(hd) + mask[:, None, None, :]
+    p = torch.softmax(s, -1)
+    return (p @ vh).permute(0, 2, 1, 3).reshape(B, Lq, D), p
+
+
+@pytest.mark.parametrize("lq,lk,nh,hd", [(36, 36, 12, 64), (128, 128, 12, 64), (37, 37, 8, 128), (36, 37, 8, 128),
+                                         (37, 128, 8, 128), (128, 36, 8, 96), (36, 128, 8, 96)])
+def test_attention(dev, lq, lk, nh, hd):
+    from k3m_amd import ops
+    B = 5
+    D = nh * hd
+    qkv_q = torch.randn(B * lq, 3 * D, device=dev)
+    qkv_k = torch.randn(B * lk, 3 * D, device=dev)
+    q, k, v = qkv_q[:, :D], qkv_k[:, D:2 * D], qkv_k[:, 2 * D:]
+    m = torch.ones(B, lk, device=dev)
+    m[:, lk - 3:] = 0
+    mask = ((1 - m) * -10000).contiguous()
+    ctx = torch.empty(B * lq, D, device=dev)
+    probs = torch.empty(B * nh * lq * lk, device=dev)
+    ops.attn_fwd(q, k, v, mask, ctx, probs, B, lq, lk, nh, hd, 1 / math.sqrt(hd), 0.0, 0, 0)
+    qr, kr, vr = [t.reshape(B, -1, D).clone().requires_grad_(True) for t in (q, k, v)]
+    cr, pr = _attn_ref(qr, kr, vr, mask, nh)
+    assert _rel(ctx.view(B, lq, D), cr) < 1e-5
+    assert _rel(probs.view(B, nh, lq, lk), pr) < 1e-5
+    dctx = torch.randn(B * lq, D, device=dev)
+    cr.backward(dctx.view(B, lq, D))
+    dq = torch.empty(B * lq, D, device=dev)
+    dk = torch.empty(B * lk, D, device=dev)
+    dv = torch.empty(B * lk, D, device=dev)
+    ops.attn_bwd(dctx, q, k, v, probs, dq, dk, dv, B, lq, lk, nh, hd, 1 / math.sqrt(hd), 0.0, 0, 0)
+    assert _rel(dq.view(B, lq, D), qr.grad) < 1e-4
+    assert _rel(dk.view(B, lk, D), kr.grad) < 1e-4
+    assert _rel(dv.view(B, lk, D), vr.grad) < 1e-4
+
+
+def test_embedding(dev):
+    from k3m_amd import ops
+    V, H, B, Lx = 1000, 768, 4, 36
+    word = torch.randn(V, H, device=dev)
+    pos = torch.randn(512, H, device=dev)
+    typ = torch.randn(2, H, device=dev)
+    g = 1 + 0.1 * torch.randn(H, device=dev)
+    b = 0.1 * torch.randn(H, device=dev)
+    ids = torch.randint(0, V, (B, Lx), device=dev)
+    ids[:, -5:] = 0
+    tt = torch.randint(0, 2, (B, Lx), device=dev)
+    y0, y1, xh = [torch.empty(B * Lx, H, device=dev) for _ in range(3)]
+    rs = torch.empty(B * Lx, device=dev)
+    ops.embed_fwd(ids, tt, word, pos, typ, g, b, y0, y1, None, xh, rs, 0.0, 0, 0)
+    wr, pr, tr = [t.clone().requires_grad_(True) for t in (word, pos, typ)]
+    e = torch.nn.functional.embedding(ids, wr, padding_idx=0) + pr[:Lx][None] + tr[tt]
+    ref = _ln_ref(e, g, b).reshape(B * Lx, H)
+    assert _rel(y0, ref) < 1e-5 and torch.equal(y0, y1)
+    dy = torch.randn_like(y0)
+    ref.backward(dy)
+    ds = torch.empty_like(dy)
+    dg = torch.zeros(H, device=dev)
+    db = torch.zeros(H, device=dev)
+    ops.ln_bwd(dy, xh, rs, g, ds, ds, dg, db)
+    dw = torch.zeros_like(word)
+    dp = torch.zeros_like(pos)
+    dt = torch.zeros_like(typ)
+    ops.embed_bwd(ids, tt, ds, dw, dp, dt)
+    assert _rel(dw, wr.grad) < 1e-4 and _rel(dp, pr.grad) < 1e-4 and _rel(dt, tr.grad) < 1e-4
+
+
+def test_adamw_matches_pytorch_transformers_semantics(dev):
+    from k3m_amd import _lib as L
+    from oracle.k3m_oracle import adamw_step
+    n = 4096
+    p = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev)
+    m = torch.randn(n, device=dev).abs() * 0.01
+    v = torch.rand(n, device=dev) * 0.01
+    pc, gc, mc, vc = [t.cpu().clone() for t in (p, g, m, v)]
+    L.call("k3m_adamw", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), None, n, 1e-4, 0.9, 0.98, 1e-8,
+           0.01, 3, 1.0, L.stream())
+    adamw_step(pc, gc, mc, vc, 3, 1e-4, 0.01)
+    torch.cuda.synchronize()
+    assert torch.allclose(p.cpu(), pc, rtol=1e-6, atol=1e-7)
+    assert torch.allclose(m.cpu(), mc, rtol=1e-6, atol=1e-8)
+    assert torch.allclose(v.cpu(), vc, rtol=1e-6, atol=1e-9)
