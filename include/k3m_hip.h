@@ -197,9 +197,11 @@ int k3m_sa_gather_bwd(const float* dX, const int64_t* index_p, const int64_t* in
 /* pytorch_transformers 1.1.0 AdamW (train_concap_struc.py:436-441) over a contiguous segment of
  * the flat parameter buffer: m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
  * p -= lr*sqrt(1-b2^t)/(1-b1^t) * m/(sqrt(v)+eps); p -= lr*wd*p.  Optionally writes a bf16 copy
- * of the updated parameters (p_bf16 may be NULL).  grad_scale multiplies g (1/world_size). */
-int k3m_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, long long n, float lr, float beta1,
-              float beta2, float eps, float wd, int step, float grad_scale, hipStream_t stream);
+ * of the updated parameters (p_bf16 may be NULL).  grad_scale multiplies g (1/world_size).
+ * Hyper-parameters are doubles, as the reference's Python floats: every derived scalar
+ * (1-beta, the bias-corrected step size, lr*wd) is formed in double and rounded once to fp32. */
+int k3m_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, long long n, double lr, double beta1,
+              double beta2, double eps, double wd, int step, float grad_scale, hipStream_t stream);
 
 /* Cast helpers for the mixed-precision path. */
 int k3m_cast_f32_bf16(const float* x, uint16_t* y, long long n, hipStream_t stream);

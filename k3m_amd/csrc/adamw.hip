@@ -21,14 +21,14 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
     for (int q = 0; q < 4; ++q) {
       const float gr = gg[q] * gscale;
       // exp_avg.mul_(beta1).add_(1 - beta1, grad)
-      mm[q] = mm[q] * b1 + omb1 * gr;
+      mm[q] = __fadd_rn(__fmul_rn(mm[q], b1), __fmul_rn(omb1, gr));
       // exp_avg_sq.mul_(beta2).addcmul_(1 - beta2, grad, grad)
-      vv[q] = vv[q] * b2 + omb2 * gr * gr;
+      vv[q] = __fadd_rn(__fmul_rn(vv[q], b2), __fmul_rn(__fmul_rn(omb2, gr), gr));
       // denom = exp_avg_sq.sqrt().add_(eps); p.addcdiv_(-step_size, exp_avg, denom)
       const float denom = sqrtf(vv[q]) + eps;
-      pp[q] = pp[q] + (-step_size) * (mm[q] / denom);
+      pp[q] = __fadd_rn(pp[q], __fmul_rn(-step_size, __fdiv_rn(mm[q], denom)));
       // p.add_(-lr * weight_decay, p)
-      if (decay != 0.f) pp[q] = pp[q] + (-decay) * pp[q];
+      if (decay != 0.f) pp[q] = __fadd_rn(pp[q], __fmul_rn(-decay, pp[q]));
     }
     reinterpret_cast<floatx4*>(p)[i] = pp;
     reinterpret_cast<floatx4*>(m)[i] = mm;
@@ -44,18 +44,18 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
 
 }  // namespace
 
-extern "C" int k3m_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, long long n, float lr,
-                         float beta1, float beta2, float eps, float wd, int step, float grad_scale, hipStream_t st) {
+extern "C" int k3m_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, long long n, double lr,
+                         double beta1, double beta2, double eps, double wd, int step, float grad_scale, hipStream_t st) {
   K3M_ARG(p && g && m && v && n >= 0 && n % 4 == 0 && step >= 1);
   K3M_ARG(((uintptr_t)p & 15) == 0 && ((uintptr_t)g & 15) == 0 && ((uintptr_t)m & 15) == 0 && ((uintptr_t)v & 15) == 0);
   if (n == 0) return 0;
-  const double bc1 = 1.0 - std::pow((double)beta1, step), bc2 = 1.0 - std::pow((double)beta2, step);
-  const float step_size = (float)((double)lr * std::sqrt(bc2) / bc1);
-  const float decay = wd > 0.f ? (float)((double)lr * (double)wd) : 0.f;
+  const double bc1 = 1.0 - std::pow(beta1, step), bc2 = 1.0 - std::pow(beta2, step);
+  const float step_size = (float)(lr * std::sqrt(bc2) / bc1);
+  const float decay = wd > 0.0 ? (float)(lr * wd) : 0.f;
   const long long n4 = n / 4;
   const int blocks = (int)std::min<long long>((n4 + 255) / 256, 256 * 16);
-  hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, st, p, g, m, v, p_bf16, n4, beta1, 1.f - beta1, beta2,
-                     1.f - beta2, eps, step_size, decay, grad_scale);
+  hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, st, p, g, m, v, p_bf16, n4, (float)beta1,
+                     (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps, step_size, decay, grad_scale);
   K3M_CHECK_LAUNCH();
   return 0;
 }

@@ -59,14 +59,16 @@ def test_engine_matches_reference_golden(dev, case):
             if k.startswith("grad_slice/"):
                 gr = gr[:4] if gr.dim() == 2 else gr[:256]
             ref = g[k]
-            err = np.abs(gr.cpu().numpy() - ref).max() / (np.abs(ref).max() + 1e-12)
-            assert err < 5e-3, (n, err)
+            # relative to the tensor's scale; absolute floor for gradients that are analytically ~0
+            # (e.g. struc_w2.bias: a softmax is shift invariant, so its true gradient is 0)
+            err = np.abs(gr.cpu().numpy() - ref).max()
+            assert err <= 5e-3 * np.abs(ref).max() + 1e-6, (n, err, np.abs(ref).max())
     for n, ref in zip(list(g["grad_norm_names"]), g["grad_norms"]):
         gn = float(G[n].double().norm())
         if np.isnan(ref):
             assert gn == 0.0, n
         else:
-            assert abs(gn - ref) <= 5e-3 * ref + 1e-7, (n, gn, ref)
+            assert abs(gn - ref) <= 5e-3 * ref + 1e-6, (n, gn, ref)
 
 
 def test_train_mode_step_is_finite_and_learns(dev):
