@@ -55,10 +55,10 @@ __device__ __forceinline__ float k3m_dropout_scale(uint64_t seed, uint64_t ctr, 
   float u = (float)(h >> 8) * (1.0f / 16777216.0f);
   return u >= p ? 1.f / (1.f - p) : 0.f;
 }
-// uniform in (0, 1]
+// uniform in the OPEN interval (0, 1): both log(u) and log(-log(u)) stay finite (gumbel noise)
 __device__ __forceinline__ float k3m_uniform(uint64_t seed, uint64_t ctr) {
   uint32_t h = k3m_hash(seed, ctr);
-  return ((float)(h >> 8) + 1.0f) * (1.0f / 16777216.0f);
+  return ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
 }
 
 // ---------------------------------------------------------------- reductions (wave64)
