@@ -61,7 +61,7 @@ typedef struct K3mGemm {
 int k3m_gemm(const K3mGemm* g, hipStream_t stream);
 
 /* out[c] (+)= sum_r x[r*ld + c]  — bias gradients (autograd of every Linear bias).
- * ws: >= 64*cols floats. */
+ * ws: >= 256*cols floats. */
 int k3m_colsum(const void* x, long long ld, int rows, int cols, float* out, int accumulate, float* ws,
                int dtype, hipStream_t stream);
 
@@ -99,10 +99,12 @@ int k3m_embed_bwd(const int64_t* ids, const int64_t* tt, const void* ds, float* 
 int k3m_attn_fwd(const void* q, long long ldq, const void* k, long long ldk, const void* v, long long ldv,
                  const float* kmask, void* ctx, long long ldc, float* probs, int nseq, int lq, int lk, int nh, int hd,
                  float scale, float p_drop, uint64_t seed, uint64_t off, int dtype, hipStream_t stream);
-int k3m_attn_bwd(const void* dctx, long long ldc, const void* q, long long ldq, const void* k, long long ldk,
-                 const void* v, long long ldv, const float* probs, void* dq, void* dk, void* dv, long long lddq,
-                 long long lddk, long long lddv, int nseq, int lq, int lk, int nh, int hd, float scale, float p_drop,
-                 uint64_t seed, uint64_t off, int dtype, hipStream_t stream);
+/* Backward (matrix cores): o = the forward context (D_i = dO_i . O_i replaces the per-row
+ * sum_j P dP reduction).  hd must be a multiple of 32. */
+int k3m_attn_bwd(const void* dctx, long long ldc, const void* o, long long ldo, const void* q, long long ldq,
+                 const void* k, long long ldk, const void* v, long long ldv, const float* probs, void* dq, void* dk,
+                 void* dv, long long lddq, long long lddk, long long lddv, int nseq, int lq, int lk, int nh, int hd,
+                 float scale, float p_drop, uint64_t seed, uint64_t off, int dtype, hipStream_t stream);
 
 /* Elementwise: out = g * gelu'(pre) (backward of the MLM/image head transforms :1795-1818). */
 int k3m_dgelu(const void* g, const void* pre, void* out, long long n, int dtype, hipStream_t stream);

@@ -57,8 +57,10 @@ __device__ __forceinline__ float k3m_dropout_scale(uint64_t seed, uint64_t ctr, 
 }
 // uniform in the OPEN interval (0, 1): both log(u) and log(-log(u)) stay finite (gumbel noise)
 __device__ __forceinline__ float k3m_uniform(uint64_t seed, uint64_t ctr) {
+  // 23 random bits: (k + 0.5) * 2^-23 is exact in fp32, so u lies in [2^-24, 1 - 2^-24] and never
+  // rounds to 1 (a 24-bit (k + 0.5) * 2^-24 rounds to exactly 1.0 for k = 2^24 - 1).
   uint32_t h = k3m_hash(seed, ctr);
-  return ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+  return ((float)(h >> 9) + 0.5f) * (1.0f / 8388608.0f);
 }
 
 // ---------------------------------------------------------------- reductions (wave64)

@@ -4,7 +4,8 @@
 
 namespace {
 
-constexpr int MAXV = 4;  // float4 chunks per lane: cols <= 64*4*4 = 1024
+constexpr int MAXV = 4;                // float4 chunks per lane: cols <= 64*4*4 = 1024
+constexpr int K3M_COLSUM_SLABS = 256;  // row chunks of the column-sum first pass
 
 template <typename T>
 __device__ __forceinline__ floatx4 ld4(const T* p);
@@ -167,13 +168,23 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   }
 }
 
+// out[c] (+)= sum_k ws[k][c]: 32 columns x 8 partial sums per workgroup (latency-bound otherwise)
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ ws, int nslab, int cols,
                                                        float* __restrict__ out, int accumulate) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
+  __shared__ float part[8][33];
+  const int cx = threadIdx.x & 31, ky = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cx;
   float s = 0.f;
-  for (int k = 0; k < nslab; ++k) s += ws[(long long)k * cols + c];
-  out[c] = accumulate ? out[c] + s : s;
+  if (c < cols)
+    for (int k = ky; k < nslab; k += 8) s += ws[(long long)k * cols + c];
+  part[ky][cx] = s;
+  __syncthreads();
+  if (ky == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += part[k][cx];
+    out[c] = accumulate ? out[c] + t : t;
+  }
 }
 
 // ------------------------------------------------------------------ embeddings
@@ -331,8 +342,8 @@ extern "C" int k3m_ln_bwd(const void* dy, const void* xhat, const float* rstd, c
                                        gamma, (T*)dres, (T*)dx, ws, rows, cols, p_in, p_out, seed, off_in, off_out,
                                        acc_res));
   K3M_CHECK_LAUNCH();
-  hipLaunchKernelGGL(slab_sum_kernel, dim3(k3m_cdiv(cols, 256)), dim3(256), 0, st, ws, nb, cols, dgamma, 1);
-  hipLaunchKernelGGL(slab_sum_kernel, dim3(k3m_cdiv(cols, 256)), dim3(256), 0, st, ws + (long long)nb * cols, nb, cols,
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(k3m_cdiv(cols, 32)), dim3(256), 0, st, ws, nb, cols, dgamma, 1);
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(k3m_cdiv(cols, 32)), dim3(256), 0, st, ws + (long long)nb * cols, nb, cols,
                      dbeta, 1);
   K3M_CHECK_LAUNCH();
   return 0;
@@ -368,10 +379,10 @@ extern "C" int k3m_colsum(const void* x, long long ld, int rows, int cols, float
                           int dtype, hipStream_t st) {
   K3M_ARG(x && out && ws && rows >= 0 && cols >= 0);
   if (cols == 0) return 0;
-  const int chunks = std::max(1, std::min(64, k3m_cdiv(rows, 64)));
+  const int chunks = std::max(1, std::min(K3M_COLSUM_SLABS, k3m_cdiv(rows, 32)));
   DISPATCH_T(dtype, hipLaunchKernelGGL(colsum_kernel<T>, dim3(k3m_cdiv(cols, 256), chunks), dim3(256), 0, st,
                                        (const T*)x, ld, rows, cols, ws));
-  hipLaunchKernelGGL(slab_sum_kernel, dim3(k3m_cdiv(cols, 256)), dim3(256), 0, st, ws, chunks, cols, out, accumulate);
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(k3m_cdiv(cols, 32)), dim3(256), 0, st, ws, chunks, cols, out, accumulate);
   K3M_CHECK_LAUNCH();
   return 0;
 }

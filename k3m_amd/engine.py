@@ -178,9 +178,9 @@ def _attn_fwd(q, k, v, mask, nseq, lq, lk, nh, p, rng, out=None):
     return ctx, (probs, nseq, lq, lk, nh, hd, p, rng.seed, off)
 
 
-def _attn_bwd(dctx, q, k, v, saved, dq, dk, dv):
+def _attn_bwd(dctx, o, q, k, v, saved, dq, dk, dv):
     probs, nseq, lq, lk, nh, hd, p, seed, off = saved
-    ops.attn_bwd(dctx, q, k, v, probs, dq, dk, dv, nseq, lq, lk, nh, hd, 1.0 / math.sqrt(hd), p, seed, off)
+    ops.attn_bwd(dctx, o, q, k, v, probs, dq, dk, dv, nseq, lq, lk, nh, hd, 1.0 / math.sqrt(hd), p, seed, off)
 
 
 class BertLayerOp(object):
@@ -221,7 +221,7 @@ class BertLayerOp(object):
         dqkv = torch.empty_like(qkv)
         for (r0, nseq, ln, mask), s in zip(segs, asv):
             r1 = r0 + nseq * ln
-            _attn_bwd(dctx[r0:r1], qkv[r0:r1, 0:H], qkv[r0:r1, H:2 * H], qkv[r0:r1, 2 * H:], s,
+            _attn_bwd(dctx[r0:r1], ctx[r0:r1], qkv[r0:r1, 0:H], qkv[r0:r1, H:2 * H], qkv[r0:r1, 2 * H:], s,
                       dqkv[r0:r1, 0:H], dqkv[r0:r1, H:2 * H], dqkv[r0:r1, 2 * H:])
         self.qkv.wgrad(dqkv, x)
         self.qkv.dgrad(dqkv, dx=dx, beta=1.0)
@@ -269,9 +269,9 @@ class ConnectionOp(object):
         dctx1 = self.d2.dgrad(da2)
         dq1 = torch.empty_like(q1)
         dq2 = torch.empty_like(q2)
-        _attn_bwd(dctx1, q2[:, 0:Hb], q1[:, Hb:2 * Hb], q1[:, 2 * Hb:], a1s, dq2[:, 0:Hb], dq1[:, Hb:2 * Hb],
+        _attn_bwd(dctx1, ctx1, q2[:, 0:Hb], q1[:, Hb:2 * Hb], q1[:, 2 * Hb:], a1s, dq2[:, 0:Hb], dq1[:, Hb:2 * Hb],
                   dq1[:, 2 * Hb:])
-        _attn_bwd(dctx2, q1[:, 0:Hb], q2[:, Hb:2 * Hb], q2[:, 2 * Hb:], a2s, dq1[:, 0:Hb], dq2[:, Hb:2 * Hb],
+        _attn_bwd(dctx2, ctx2, q1[:, 0:Hb], q2[:, Hb:2 * Hb], q2[:, 2 * Hb:], a2s, dq1[:, 0:Hb], dq2[:, Hb:2 * Hb],
                   dq2[:, 2 * Hb:])
         self.qkv1.wgrad(dq1, s1)
         self.qkv1.dgrad(dq1, dx=ds1, beta=1.0)

@@ -79,7 +79,7 @@ def linear_wgrad(dy, x, gW, gb=None, alpha=1.0):
 
 def colsum(x, out, accumulate=True, alpha=1.0):
     rows, cols = x.shape
-    ws = torch.empty((64 * cols,), dtype=torch.float32, device=x.device)
+    ws = torch.empty((256 * cols,), dtype=torch.float32, device=x.device)
     if alpha == 1.0:
         call("k3m_colsum", ptr(x), _ld(x), rows, cols, ptr(out), int(accumulate), ptr(ws), dt(x), stream())
     else:
@@ -127,8 +127,8 @@ def attn_fwd(q, k, v, kmask, ctx, probs, nseq, lq, lk, nh, hd, scale, p_drop, se
          nseq, lq, lk, nh, hd, scale, p_drop, seed, off, dt(ctx), stream())
 
 
-def attn_bwd(dctx, q, k, v, probs, dq, dk, dv, nseq, lq, lk, nh, hd, scale, p_drop, seed, off):
-    call("k3m_attn_bwd", ptr(dctx), _ld(dctx), ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v), ptr(probs), ptr(dq),
+def attn_bwd(dctx, o, q, k, v, probs, dq, dk, dv, nseq, lq, lk, nh, hd, scale, p_drop, seed, off):
+    call("k3m_attn_bwd", ptr(dctx), _ld(dctx), ptr(o), _ld(o), ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v), ptr(probs), ptr(dq),
          ptr(dk), ptr(dv), _ld(dq), _ld(dk), _ld(dv), nseq, lq, lk, nh, hd, scale, p_drop, seed, off, dt(dctx),
          stream())
 

@@ -176,7 +176,7 @@ def test_attention(dev, lq, lk, nh, hd):
     dq = torch.empty(B * lq, D, device=dev)
     dk = torch.empty(B * lk, D, device=dev)
     dv = torch.empty(B * lk, D, device=dev)
-    ops.attn_bwd(dctx, q, k, v, probs, dq, dk, dv, B, lq, lk, nh, hd, 1 / math.sqrt(hd), 0.0, 0, 0)
+    ops.attn_bwd(dctx, ctx, q, k, v, probs, dq, dk, dv, B, lq, lk, nh, hd, 1 / math.sqrt(hd), 0.0, 0, 0)
     assert _rel(dq.view(B, lq, D), qr.grad) < 1e-4
     assert _rel(dk.view(B, lk, D), kr.grad) < 1e-4
     assert _rel(dv.view(B, lk, D), vr.grad) < 1e-4
