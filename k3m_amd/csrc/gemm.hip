@@ -17,11 +17,11 @@
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
-constexpr int LDSA = BM + 4, LDSB = BN + 4;
 
 // Load one operand tile (BK x TILE) for k0.. into 4 float4 registers per thread.
 // KC = operand is K-contiguous in memory (element (mn, k) at p[mn*ld + k]); else MN-contiguous
-// (element (mn, k) at p[k*ld + mn]).
+// (element (mn, k) at p[k*ld + mn]).  Both map 8 consecutive lanes onto one contiguous 128-byte
+// segment, so every wave instruction touches whole cache lines.
 template <bool KC, bool VEC, int TILE>
 __device__ __forceinline__ void load_tile(const float* __restrict__ p, long long ld, int mn0, int k0, int MN, int K,
                                           floatx4 (&r)[4]) {
@@ -29,8 +29,9 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ p, long long
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
     if constexpr (KC) {
-      const int mn = t & (TILE - 1);
-      const int kq = (t >> 7) + 2 * it;  // 0..7
+      const int idx = t + 256 * it;
+      const int mn = idx >> 3;          // 0..127
+      const int kq = idx & 7;           // float4 index along k
       const int gm = mn0 + mn, gk = k0 + kq * 4;
       if constexpr (VEC) {
         if (gm < MN && gk < K) {
@@ -60,14 +61,20 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ p, long long
   }
 }
 
-template <bool KC, int TILE, int LDST>
+// LDS row stride (floats) of the k-major image [BK][TILE + pad]: odd for the transposing scalar
+// writes of K-contiguous operands (conflict-free), a multiple of 4 for float4 writes otherwise.
+template <bool KC, int TILE>
+constexpr int lds_stride() { return KC ? TILE + 1 : TILE + 4; }
+
+template <bool KC, int TILE>
 __device__ __forceinline__ void store_tile(float* __restrict__ s, const floatx4 (&r)[4]) {
+  constexpr int LDST = lds_stride<KC, TILE>();
   const int t = threadIdx.x;
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
     if constexpr (KC) {
-      const int mn = t & (TILE - 1);
-      const int kq = (t >> 7) + 2 * it;
+      const int idx = t + 256 * it;
+      const int mn = idx >> 3, kq = idx & 7;
 #pragma unroll
       for (int q = 0; q < 4; ++q) s[(kq * 4 + q) * LDST + mn] = r[it][q];
     } else {
@@ -87,6 +94,7 @@ __device__ __forceinline__ int xcd_remap(int id, int nblk) {
 
 template <bool AK, bool BK_, bool AV, bool BV, int EPI>
 __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(K3mGemm g) {
+  constexpr int LDSA = lds_stride<AK, BM>(), LDSB = lds_stride<BK_, BN>();
   __shared__ float As[2][BK * LDSA];
   __shared__ float Bs[2][BK * LDSB];
   const int M = g.m, N = g.n, K = g.k;
@@ -128,8 +136,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(K3mGemm g) {
   if (nk > 0) {
     load_tile<AK, AV, BM>(A, g.lda, m0, kbeg, M, kend, ra);
     load_tile<BK_, BV, BN>(B, g.ldb, n0, kbeg, N, kend, rb);
-    store_tile<AK, BM, LDSA>(As[0], ra);
-    store_tile<BK_, BN, LDSB>(Bs[0], rb);
+    store_tile<AK, BM>(As[0], ra);
+    store_tile<BK_, BN>(Bs[0], rb);
   }
   __syncthreads();
   const int kl = lane >> 5, cl = lane & 31;
@@ -155,8 +163,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(K3mGemm g) {
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
     }
     if (more) {
-      store_tile<AK, BM, LDSA>(As[cur ^ 1], ra);
-      store_tile<BK_, BN, LDSB>(Bs[cur ^ 1], rb);
+      store_tile<AK, BM>(As[cur ^ 1], ra);
+      store_tile<BK_, BN>(Bs[cur ^ 1], rb);
     }
     __syncthreads();
   }
