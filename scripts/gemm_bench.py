@@ -1,0 +1,67 @@
+"""Microbenchmark of the libk3m_hip GEMM on the text-layer shapes of the wide engine (bs=64):
+forward x.W^T, input-gradient dY.W and weight-gradient dY^T.X.  Prints TF/s per shape."""
+import sys
+import os
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from k3m_amd import ops, _lib as L  # noqa: E402
+
+M = 20992
+SHAPES = [
+    ("fwd qkv", "nt", M, 2304, 768, L.EPI_BIAS),
+    ("fwd out", "nt", M, 768, 768, L.EPI_BIAS),
+    ("fwd ffn1 gelu", "nt", M, 3072, 768, L.EPI_BIAS_GELU),
+    ("fwd ffn2", "nt", M, 768, 3072, L.EPI_BIAS),
+    ("dgrad qkv", "nn", M, 768, 2304, L.EPI_NONE),
+    ("dgrad ffn2->dgelu", "nn", M, 3072, 768, L.EPI_DGELU),
+    ("dgrad ffn1", "nn", M, 768, 3072, L.EPI_NONE),
+    ("wgrad ffn1", "tn", 3072, 768, M, L.EPI_NONE),
+    ("wgrad ffn2", "tn", 768, 3072, M, L.EPI_NONE),
+    ("wgrad qkv", "tn", 2304, 768, M, L.EPI_NONE),
+    ("wgrad out", "tn", 768, 768, M, L.EPI_NONE),
+]
+
+
+def run(name, kind, m, n, k, epi, reps=10):
+    dev = torch.device("cuda")
+    if kind == "nt":
+        a, b = torch.randn(m, k, device=dev), torch.randn(n, k, device=dev) * 0.02
+        at, bt = 0, 1
+    elif kind == "nn":
+        a, b = torch.randn(m, k, device=dev), torch.randn(k, n, device=dev) * 0.02
+        at, bt = 0, 0
+    else:
+        a, b = torch.randn(k, m, device=dev), torch.randn(k, n, device=dev) * 0.02
+        at, bt = 1, 0
+    c = torch.zeros(m, n, device=dev)
+    bias = torch.zeros(n, device=dev)
+    aux = torch.randn(m, n, device=dev) if epi in (L.EPI_BIAS_GELU, L.EPI_DGELU) else None
+    beta = 1.0 if kind == "tn" else 0.0
+    s = ops._splitk(m, n, k) if kind == "tn" else 1
+    ws = torch.empty(s * m * n, device=dev) if s > 1 else None
+
+    def go():
+        ops.gemm(a, at, b, bt, c, m, n, k, epi, bias if epi in (L.EPI_BIAS, L.EPI_BIAS_GELU) else None, aux, 1.0,
+                 beta, s, ws)
+    for _ in range(3):
+        go()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        go()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    tf = 2.0 * m * n * k / (ms * 1e-3) / 1e12
+    print("%-20s %s m=%6d n=%5d k=%6d splitk=%2d  %8.3f ms  %6.1f TF/s" % (name, kind, m, n, k, s, ms, tf), flush=True)
+    return tf
+
+
+if __name__ == "__main__":
+    L.load()
+    tot_ms = 0
+    for sh in SHAPES:
+        run(*sh)

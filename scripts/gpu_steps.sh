@@ -25,6 +25,7 @@ for s in "$@"; do
     bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
     benchq) step bench 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     prof) export TMPDIR=/tmp; step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    gemm) step gemm 300 python scripts/gemm_bench.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
