@@ -21,6 +21,13 @@ SHAPES = [
     ("wgrad ffn2", "tn", 768, 3072, M, L.EPI_NONE),
     ("wgrad qkv", "tn", 2304, 768, M, L.EPI_NONE),
     ("wgrad out", "tn", 768, 768, M, L.EPI_NONE),
+    # co-attention (per-pass) shapes
+    ("co txt ffn2", "nt", 2304, 768, 3072, L.EPI_BIAS),
+    ("co img qkv", "nt", 2368, 3072, 1024, L.EPI_BIAS),
+    ("co img dense", "nt", 2368, 1024, 1024, L.EPI_BIAS),
+    ("co pv ffn1", "nt", 8192, 3072, 768, L.EPI_BIAS_GELU),
+    ("co txt dgrad", "nn", 2304, 768, 3072, L.EPI_NONE),
+    ("co img wgrad", "tn", 1024, 1024, 2368, L.EPI_NONE),
 ]
 
 
