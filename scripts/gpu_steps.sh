@@ -26,6 +26,7 @@ for s in "$@"; do
     benchq) step bench 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     prof) export TMPDIR=/tmp; step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     gemm) step gemm 300 python scripts/gemm_bench.py ;;
+    ddp2) step ddp2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --backend gloo --batch 16 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
