@@ -69,6 +69,8 @@ def run(name, kind, m, n, k, epi, reps=10):
 
 if __name__ == "__main__":
     L.load()
-    tot_ms = 0
+    only = sys.argv[1] if len(sys.argv) > 1 else None
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     for sh in SHAPES:
-        run(*sh)
+        if only is None or sh[0] == only:
+            run(*sh, reps=reps)
