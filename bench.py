@@ -74,6 +74,20 @@ class GemmProbe(object):
         return sum(s.elapsed_time(e) for s, e in self.events) / len(self.events)
 
 
+def pmc_traffic(key, kernel_prefix):
+    """HBM-side bytes per launch of the probed GEMM, from the committed rocprofv3 PMC passes
+    (profiles/r1_gemm_ffn1_pmc.json: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), or None."""
+    path = os.path.join(HERE, "profiles", "r1_gemm_ffn1_pmc.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if tuple(d.get("shape", ())) != tuple(key) or not d.get("kernel", "").startswith(kernel_prefix):
+        return None
+    return int(d["traffic_bytes"])
+
+
 def cpu_baseline(cfg, bsz, steps):
     """Oracle (torch CPU fp32) fwd+bwd+AdamW on a bounded sample; baseline only."""
     from oracle import k3m_oracle as O
@@ -190,7 +204,9 @@ def main():
                      "peak": PEAK_F32_MFMA / 1e12, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_F32_MFMA, 4) if achieved else None,
                      "avg_launch_ms": round(gemm_ms, 4) if gemm_ms else None,
-                     "launches": len(probe.events), "traffic": None},
+                     "launches": len(probe.events),
+                     "traffic": pmc_traffic(probe.key, "void (anonymous namespace)::gemm_f32_kernel"),
+                     "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/r1_gemm_ffn1_pmc.json)"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
