@@ -47,8 +47,9 @@ typedef struct K3mGemm {
   int m, n, k;
   int a_trans, b_trans;
   int epilogue;
-  int dtype;
+  int dtype;             /* operand (A, B) type: K3M_F32, or K3M_BF16 (fp32 accumulation)       */
   int splitk;            /* >1: K split over splitk workgroup slices (epilogue must be NONE);   */
+  int c_dtype;           /* C and aux type: K3M_F32 (K3M_F32 operands require it) or K3M_BF16   */
   long long lda, ldb, ldc, ldaux;
   const void* a;
   const void* b;

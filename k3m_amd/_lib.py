@@ -21,7 +21,7 @@ vp, i32, i64, f32, u64 = C.c_void_p, C.c_int, C.c_longlong, C.c_float, C.c_uint6
 
 class K3mGemm(C.Structure):
     _fields_ = [("m", i32), ("n", i32), ("k", i32), ("a_trans", i32), ("b_trans", i32), ("epilogue", i32),
-                ("dtype", i32), ("splitk", i32), ("lda", i64), ("ldb", i64), ("ldc", i64), ("ldaux", i64),
+                ("dtype", i32), ("splitk", i32), ("c_dtype", i32), ("lda", i64), ("ldb", i64), ("ldc", i64), ("ldaux", i64),
                 ("a", vp), ("b", vp), ("c", vp), ("bias", vp), ("aux", vp), ("ws", vp), ("alpha", f32),
                 ("beta", f32)]
 

@@ -28,13 +28,9 @@ __device__ __forceinline__ float to_f(bf16_t v) { return __uint_as_float(((uint3
 template <typename T> __device__ __forceinline__ T from_f(float v);
 template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
 template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float v) {
-  uint32_t u = __float_as_uint(v);
+  // round to nearest even; hipcc emits v_cvt_pk_bf16_f32, which keeps a NaN a NaN
   bf16_t r;
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) {
-    r.x = (uint16_t)((u >> 16) | 0x40);  // keep NaN a NaN
-  } else {
-    r.x = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);  // round to nearest even
-  }
+  r.x = __builtin_bit_cast(uint16_t, (__bf16)v);
   return r;
 }
 

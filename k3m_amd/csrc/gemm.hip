@@ -265,16 +265,20 @@ long long nblocks(const K3mGemm& g, int bm, int bn) {
 
 }  // namespace
 
+int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st);  // gemm_bf16.hip
+
 extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
   if (!gp) return K3M_EINVAL;
   const K3mGemm& g = *gp;
   K3M_ARG(g.m >= 0 && g.n >= 0 && g.k >= 0);
   if (g.m == 0 || g.n == 0) return 0;
-  K3M_ARG(g.dtype == K3M_F32);
+  K3M_ARG(g.dtype == K3M_F32 || g.dtype == K3M_BF16);
+  K3M_ARG(g.c_dtype == K3M_F32 || (g.dtype == K3M_BF16 && g.c_dtype == K3M_BF16));
   K3M_ARG(g.a && g.b && g.c);
   K3M_ARG(g.splitk <= 1 || (g.epilogue == K3M_EPI_NONE && g.ws));
   K3M_ARG(g.epilogue == K3M_EPI_NONE || g.epilogue == K3M_EPI_DGELU || g.bias);
   K3M_ARG((g.epilogue != K3M_EPI_BIAS_GELU && g.epilogue != K3M_EPI_DGELU) || g.aux);
+  if (g.dtype == K3M_BF16) return k3m_gemm_bf16_impl(g, st);
   // A: K-contiguous iff a_trans == 0; B: K-contiguous iff b_trans == 1
   const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
   const bool av = aligned16(g.a) && (g.lda % 4 == 0) && ((ak ? g.k : g.m) % 4 == 0);

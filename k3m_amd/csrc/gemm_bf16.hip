@@ -1,0 +1,384 @@
+// bf16 MFMA GEMM for gfx950 (mixed precision: bf16 operands, fp32 accumulation, fp32 or bf16 C).
+//
+// v_mfma_f32_32x32x16_bf16 (2.5 PF/s dense peak): 128x128x64 block tile (64x128 / 64x64 for the
+// small co-attention GEMMs), 4 waves in 2x2, each wave owning up to 2x2 MFMA tiles of 32x32.
+//
+// LDS image of an operand tile is [TILE][64] bf16 with K contiguous (128-B rows): one MFMA operand
+// fragment is one ds_read_b128 (lane l reads row l&31, k-chunk 2*ks + (l>>5)).  The 16-B chunk c of
+// row r is stored in slot c ^ ((r >> 1) & 7), which puts each 16-lane ds_read_b128 group
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...) on 16 distinct (row parity, slot) bank quads:
+// conflict-free reads (a plain [128][64] image is 8-way).
+//
+// Staging (register double buffer, one barrier per K-tile):
+//   * K-contiguous operands (activations, torch Linear weights for x.W^T): 8 lanes per 128-B row,
+//     written to LDS as-is (ds_write_b128);
+//   * MN-contiguous operands (W for input gradients, dY^T and X for weight gradients): each thread
+//     loads a 4(k) x 8(mn) block as four 16-B row pieces, transposes it in registers (16-bit
+//     permutes) and writes eight 8-B k-runs (ds_write_b64) into the same K-contiguous image.
+// Split-K writes fp32 slabs, reduced deterministically by a second kernel (weight gradients).
+#include "common.h"
+
+namespace {
+
+constexpr int BK = 64, NT = 256;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// element offset (bf16 units) of k-chunk c (8 bf16) of row r in a swizzled [TILE][64] image
+__device__ __forceinline__ int swz(int r, int c) { return r * BK + ((c ^ ((r >> 1) & 7)) << 3); }
+
+__device__ __forceinline__ uint32_t lo_pair(uint32_t a, uint32_t b) { return (a & 0xffffu) | (b << 16); }
+__device__ __forceinline__ uint32_t hi_pair(uint32_t a, uint32_t b) { return (a >> 16) | (b & 0xffff0000u); }
+
+template <bool KC, int TILE>
+struct Stage {
+  static constexpr int NR = KC ? TILE / 32 : 4;
+  u32x4 r[NR];
+};
+
+// Load the (TILE x BK) tile at (mn0, k0) into registers.
+template <bool KC, bool VEC, int TILE>
+__device__ __forceinline__ void load_tile(const uint16_t* __restrict__ p, long long ld, int mn0, int k0, int MN,
+                                          int K, Stage<KC, TILE>& s) {
+  const int t = threadIdx.x;
+  if constexpr (KC) {
+#pragma unroll
+    for (int it = 0; it < TILE / 32; ++it) {
+      const int idx = t + NT * it;
+      const int row = idx >> 3, ch = idx & 7;
+      const int gm = mn0 + row, gk = k0 + ch * 8;
+      if constexpr (VEC) {
+        s.r[it] = (gm < MN && gk < K) ? *reinterpret_cast<const u32x4*>(p + (long long)gm * ld + gk)
+                                      : u32x4{0u, 0u, 0u, 0u};
+      } else {
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t e0 = (gm < MN && gk + 2 * q < K) ? p[(long long)gm * ld + gk + 2 * q] : 0u;
+          const uint32_t e1 = (gm < MN && gk + 2 * q + 1 < K) ? p[(long long)gm * ld + gk + 2 * q + 1] : 0u;
+          w[q] = e0 | (e1 << 16);
+        }
+        s.r[it] = u32x4{w[0], w[1], w[2], w[3]};
+      }
+    }
+  } else {
+    constexpr int G8 = TILE / 8;  // mn-groups of 8
+    if (2 * TILE < NT && t >= 2 * TILE) return;
+    const int g8 = t % G8, g4 = t / G8;
+    const int gm = mn0 + g8 * 8;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int gk = k0 + g4 * 4 + kk;
+      if constexpr (VEC) {
+        s.r[kk] = (gk < K && gm < MN) ? *reinterpret_cast<const u32x4*>(p + (long long)gk * ld + gm)
+                                      : u32x4{0u, 0u, 0u, 0u};
+      } else {
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t e0 = (gk < K && gm + 2 * q < MN) ? p[(long long)gk * ld + gm + 2 * q] : 0u;
+          const uint32_t e1 = (gk < K && gm + 2 * q + 1 < MN) ? p[(long long)gk * ld + gm + 2 * q + 1] : 0u;
+          w[q] = e0 | (e1 << 16);
+        }
+        s.r[kk] = u32x4{w[0], w[1], w[2], w[3]};
+      }
+    }
+  }
+}
+
+template <bool KC, int TILE>
+__device__ __forceinline__ void store_tile(uint16_t* __restrict__ lds, const Stage<KC, TILE>& s) {
+  const int t = threadIdx.x;
+  if constexpr (KC) {
+#pragma unroll
+    for (int it = 0; it < TILE / 32; ++it) {
+      const int idx = t + NT * it;
+      *reinterpret_cast<u32x4*>(lds + swz(idx >> 3, idx & 7)) = s.r[it];
+    }
+  } else {
+    constexpr int G8 = TILE / 8;
+    if (2 * TILE < NT && t >= 2 * TILE) return;
+    const int g8 = t % G8, g4 = t / G8;
+    const int c = g4 >> 1, half = (g4 & 1) * 4;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const int mn = g8 * 8 + 2 * w;
+      const u32x2 e = {lo_pair(s.r[0][w], s.r[1][w]), lo_pair(s.r[2][w], s.r[3][w])};
+      const u32x2 o = {hi_pair(s.r[0][w], s.r[1][w]), hi_pair(s.r[2][w], s.r[3][w])};
+      *reinterpret_cast<u32x2*>(lds + swz(mn, c) + half) = e;
+      *reinterpret_cast<u32x2*>(lds + swz(mn + 1, c) + half) = o;
+    }
+  }
+}
+
+__device__ __forceinline__ int xcd_remap(int id, int nblk) {
+  const int xcd = id & 7, q = nblk >> 3, rr = nblk & 7;
+  const int base = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
+  return base + (id >> 3);
+}
+
+// 8 consecutive elements <-> fp32 registers, as 16-B vectors (p 16-B aligned)
+__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
+  const floatx4 a = *reinterpret_cast<const floatx4*>(p), b = *reinterpret_cast<const floatx4*>(p + 4);
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+__device__ __forceinline__ void load8(const bf16_t* p, float (&v)[8]) {
+  const u32x4 a = *reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[2 * q] = __uint_as_float(a[q] << 16);
+    v[2 * q + 1] = __uint_as_float(a[q] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
+  *reinterpret_cast<floatx4*>(p) = floatx4{v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<floatx4*>(p + 4) = floatx4{v[4], v[5], v[6], v[7]};
+}
+__device__ __forceinline__ void store8(bf16_t* p, const float (&v)[8]) {
+  u32x4 a;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) a[q] = (uint32_t)from_f<bf16_t>(v[2 * q]).x | ((uint32_t)from_f<bf16_t>(v[2 * q + 1]).x << 16);
+  *reinterpret_cast<u32x4*>(p) = a;
+}
+
+template <int TBM, int TBN, bool AK, bool BK_, bool VEC, int EPI, typename CT>
+__global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(K3mGemm g) {
+  constexpr int FM = TBM / 64, FN = TBN / 64;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (TBM + TBN) * BK];
+  const int M = g.m, N = g.n, K = g.k;
+  const int tm = (M + TBM - 1) / TBM, tn = (N + TBN - 1) / TBN;
+  const int nblk = tm * tn;
+  const int id = xcd_remap(blockIdx.x, nblk);
+  constexpr int GROUP = 8;
+  const int group_sz = GROUP * tn;
+  const int gidx = id / group_sz;
+  const int first_m = gidx * GROUP;
+  const int gm_sz = min(tm - first_m, GROUP);
+  const int bm = first_m + (id % group_sz) % gm_sz;
+  const int bn = (id % group_sz) / gm_sz;
+  const int m0 = bm * TBM, n0 = bn * TBN;
+
+  int kbeg = 0, kend = K;
+  if (g.splitk > 1) {
+    const int per = ((K + g.splitk - 1) / g.splitk + BK - 1) / BK * BK;
+    kbeg = blockIdx.y * per;
+    kend = min(K, kbeg + per);
+  }
+  const uint16_t* A = static_cast<const uint16_t*>(g.a);
+  const uint16_t* B = static_cast<const uint16_t*>(g.b);
+  constexpr int BUF = (TBM + TBN) * BK;  // one stage: A image [TBM][64] then B image [TBN][64]
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = (w >> 1) * (TBM / 2), wn = (w & 1) * (TBN / 2);
+  floatx16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  Stage<AK, TBM> ra;
+  Stage<BK_, TBN> rb;
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  if (nk > 0) {
+    load_tile<AK, VEC, TBM>(A, g.lda, m0, kbeg, M, kend, ra);
+    load_tile<BK_, VEC, TBN>(B, g.ldb, n0, kbeg, N, kend, rb);
+    store_tile<AK, TBM>(smem, ra);
+    store_tile<BK_, TBN>(smem + TBM * BK, rb);
+  }
+  __syncthreads();
+  const int kl = lane >> 5, cl = lane & 31;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      const int k0 = kbeg + (kt + 1) * BK;
+      load_tile<AK, VEC, TBM>(A, g.lda, m0, k0, M, kend, ra);
+      load_tile<BK_, VEC, TBN>(B, g.ldb, n0, k0, N, kend, rb);
+    }
+    const uint16_t* as = smem + cur * BUF;
+    const uint16_t* bs = as + TBM * BK;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 a[FM], b[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const bf16x8*>(as + swz(wm + 32 * i + cl, 2 * ks + kl));
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const bf16x8*>(bs + swz(wn + 32 * j + cl, 2 * ks + kl));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      store_tile<AK, TBM>(smem + (cur ^ 1) * BUF, ra);
+      store_tile<BK_, TBN>(smem + (cur ^ 1) * BUF + TBM * BK, rb);
+    }
+    __syncthreads();
+  }
+
+  // epilogue, staged through LDS (free after the last barrier) so that global traffic is row-
+  // contiguous 16-B vectors: each wave writes one 32-row slice of its accumulators (fp32) into a
+  // private [32][WN+8] region (stride = 8 mod 16 floats: the two half-waves' rows land 32 banks apart),
+  // then reads it back 8 consecutive columns per lane and applies the epilogue on the way out.
+  // acc[i][j][r] holds row (r&3) + 8*(r>>2) + 4*(lane>>5), col lane&31 of MFMA tile (i, j).
+  constexpr int WN = TBN / 2, WS = WN + 8, LPR = WN / 8, RPP = 64 / LPR;
+  static_assert(4 * 32 * WS * 4 <= 2 * (TBM + TBN) * BK * 2, "epilogue staging exceeds the LDS tile");
+  float* wl = reinterpret_cast<float*>(smem) + w * 32 * WS;
+  const bool split = g.splitk > 1;
+  CT* C = split ? reinterpret_cast<CT*>(g.ws + (long long)blockIdx.y * M * N) : static_cast<CT*>(g.c);
+  const long long ldc = split ? N : g.ldc;
+  const float alpha = split ? 1.f : g.alpha, beta = split ? 0.f : g.beta;
+  CT* aux = static_cast<CT*>(g.aux);
+  const float* bias = g.bias;
+  constexpr bool HAS_AUX = EPI == K3M_EPI_BIAS_GELU || EPI == K3M_EPI_DGELU;
+  constexpr bool HAS_BIAS = EPI == K3M_EPI_BIAS || EPI == K3M_EPI_BIAS_GELU || EPI == K3M_EPI_BIAS_SIGMOID;
+  const bool cvec = (ldc % 8 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) &&
+                    (!HAS_AUX || ((g.ldaux % 8 == 0) && ((reinterpret_cast<uintptr_t>(aux) & 15) == 0)));
+  const int lr = lane / LPR, lc = (lane % LPR) * 8;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) wl[((r & 3) + 8 * (r >> 2) + 4 * kl) * WS + 32 * j + cl] = acc[i][j][r];
+    __syncthreads();
+#pragma unroll
+    for (int ps = 0; ps < 32 / RPP; ++ps) {
+      const int rr = ps * RPP + lr;
+      const int row = m0 + wm + 32 * i + rr;
+      const int col = n0 + wn + lc;
+      const floatx4 v0 = *reinterpret_cast<const floatx4*>(wl + rr * WS + lc);
+      const floatx4 v1 = *reinterpret_cast<const floatx4*>(wl + rr * WS + lc + 4);
+      if (row >= M || col >= N) continue;
+      float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      const bool full = cvec && col + 8 <= N;
+      CT* cp = C + (long long)row * ldc + col;
+      CT* ap = HAS_AUX ? aux + (long long)row * g.ldaux + col : nullptr;
+      float old[8], ax[8], bb[8];
+      if constexpr (HAS_BIAS) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bb[e] = col + e < N ? bias[col + e] : 0.f;
+      }
+      if constexpr (EPI == K3M_EPI_DGELU) {
+        if (full) load8(ap, ax);
+        else
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ax[e] = col + e < N ? to_f(ap[e]) : 0.f;
+      }
+      const bool rd_old = (EPI == K3M_EPI_NONE || EPI == K3M_EPI_BIAS || EPI == K3M_EPI_DGELU) && beta != 0.f;
+      if (rd_old) {
+        if (full) load8(cp, old);
+        else
+#pragma unroll
+          for (int e = 0; e < 8; ++e) old[e] = col + e < N ? to_f(cp[e]) : 0.f;
+      }
+      float o[8], pa[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if constexpr (EPI == K3M_EPI_NONE) {
+          o[e] = alpha * v[e];
+        } else if constexpr (EPI == K3M_EPI_BIAS) {
+          o[e] = alpha * (v[e] + bb[e]);
+        } else if constexpr (EPI == K3M_EPI_BIAS_GELU) {
+          pa[e] = v[e] + bb[e];
+          o[e] = gelu_f(to_f(from_f<CT>(pa[e])));  // gelu of the stored pre-activation the backward sees
+        } else if constexpr (EPI == K3M_EPI_DGELU) {
+          o[e] = alpha * v[e] * dgelu_f(ax[e]);
+        } else {
+          o[e] = sigmoid_f(v[e] + bb[e]);
+        }
+        if (rd_old) o[e] += beta * old[e];
+      }
+      if (full) {
+        store8(cp, o);
+        if constexpr (EPI == K3M_EPI_BIAS_GELU) store8(ap, pa);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (col + e < N) {
+            cp[e] = from_f<CT>(o[e]);
+            if constexpr (EPI == K3M_EPI_BIAS_GELU) ap[e] = from_f<CT>(pa[e]);
+          }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_bf16_kernel(const float* __restrict__ ws, int splits, int M,
+                                                                 int N, float* __restrict__ C, long long ldc,
+                                                                 float alpha, float beta) {
+  const long long total = (long long)M * N;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += ws[(long long)k * total + e];
+    const int row = (int)(e / N), col = (int)(e % N);
+    float* cp = C + (long long)row * ldc + col;
+    float o = alpha * s;
+    if (beta != 0.f) o += beta * *cp;
+    *cp = o;
+  }
+}
+
+template <int TBM, int TBN, bool AK, bool BK_, bool VEC, typename CT>
+int launch_epi(const K3mGemm& g, hipStream_t st) {
+  const int tm = (g.m + TBM - 1) / TBM, tn = (g.n + TBN - 1) / TBN;
+  dim3 grid(tm * tn, g.splitk > 1 ? g.splitk : 1);
+  switch (g.epilogue) {
+#define K3M_GEMM_CASE(E) \
+    case E: hipLaunchKernelGGL((gemm_bf16_kernel<TBM, TBN, AK, BK_, VEC, E, CT>), grid, dim3(NT), 0, st, g); break;
+    K3M_GEMM_CASE(K3M_EPI_NONE)
+    K3M_GEMM_CASE(K3M_EPI_BIAS)
+    K3M_GEMM_CASE(K3M_EPI_BIAS_GELU)
+    K3M_GEMM_CASE(K3M_EPI_DGELU)
+    K3M_GEMM_CASE(K3M_EPI_BIAS_SIGMOID)
+#undef K3M_GEMM_CASE
+    default: return K3M_EINVAL;
+  }
+  return 0;
+}
+
+template <int TBM, int TBN, typename CT>
+int launch_tile(const K3mGemm& g, bool ak, bool bk, bool vec, hipStream_t st) {
+  if (ak && bk) return vec ? launch_epi<TBM, TBN, true, true, true, CT>(g, st) : launch_epi<TBM, TBN, true, true, false, CT>(g, st);
+  if (ak) return vec ? launch_epi<TBM, TBN, true, false, true, CT>(g, st) : launch_epi<TBM, TBN, true, false, false, CT>(g, st);
+  if (bk) return vec ? launch_epi<TBM, TBN, false, true, true, CT>(g, st) : launch_epi<TBM, TBN, false, true, false, CT>(g, st);
+  return vec ? launch_epi<TBM, TBN, false, false, true, CT>(g, st) : launch_epi<TBM, TBN, false, false, false, CT>(g, st);
+}
+
+template <typename CT>
+int launch_ct(const K3mGemm& g, bool ak, bool bk, bool vec, hipStream_t st) {
+  auto nb = [&](int bm, int bn) {
+    return (long long)((g.m + bm - 1) / bm) * ((g.n + bn - 1) / bn) * (g.splitk > 1 ? g.splitk : 1);
+  };
+  if (g.splitk > 1 || nb(128, 128) >= 384) return launch_tile<128, 128, CT>(g, ak, bk, vec, st);
+  if (nb(64, 128) >= 384) return launch_tile<64, 128, CT>(g, ak, bk, vec, st);
+  return launch_tile<64, 64, CT>(g, ak, bk, vec, st);
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+// Called by k3m_gemm (gemm.hip) for dtype == K3M_BF16; arguments already validated there.
+int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st) {
+  K3M_ARG(g.splitk <= 1 || g.c_dtype == K3M_F32);
+  const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
+  const bool av = aligned16(g.a) && (g.lda % 8 == 0) && ((ak ? g.k : g.m) % 8 == 0);
+  const bool bv = aligned16(g.b) && (g.ldb % 8 == 0) && ((bk ? g.k : g.n) % 8 == 0);
+  const bool vec = av && bv;
+  int rc = g.c_dtype == K3M_F32 ? launch_ct<float>(g, ak, bk, vec, st) : launch_ct<bf16_t>(g, ak, bk, vec, st);
+  if (rc) return rc;
+  K3M_CHECK_LAUNCH();
+  if (g.splitk > 1) {
+    const long long total = (long long)g.m * g.n;
+    const int blocks = (int)std::min<long long>((total + 255) / 256, 2048);
+    hipLaunchKernelGGL(splitk_reduce_bf16_kernel, dim3(blocks), dim3(256), 0, st, g.ws, g.splitk, g.m, g.n,
+                       static_cast<float*>(g.c), g.ldc, g.alpha, g.beta);
+    K3M_CHECK_LAUNCH();
+  }
+  return 0;
+}

@@ -27,7 +27,9 @@ def gemm(a, a_trans, b, b_trans, c, m, n, k, epi=L.EPI_NONE, bias=None, aux=None
     g = L.K3mGemm()
     g.m, g.n, g.k = m, n, k
     g.a_trans, g.b_trans = a_trans, b_trans
-    g.epilogue, g.dtype, g.splitk = epi, dt(c), splitk
+    assert a.dtype == b.dtype, "A and B must share a dtype"
+    assert aux is None or aux.dtype == c.dtype, "aux has the dtype of C"
+    g.epilogue, g.dtype, g.splitk, g.c_dtype = epi, dt(a), splitk, dt(c)
     g.lda, g.ldb, g.ldc = _ld(a), _ld(b), _ld(c)
     g.ldaux = _ld(aux) if aux is not None else 0
     g.a, g.b, g.c = ptr(a), ptr(b), ptr(c)

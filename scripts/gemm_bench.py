@@ -31,7 +31,7 @@ SHAPES = [
 ]
 
 
-def run(name, kind, m, n, k, epi, reps=10):
+def run(name, kind, m, n, k, epi, reps=10, dtype=torch.float32):
     dev = torch.device("cuda")
     if kind == "nt":
         a, b = torch.randn(m, k, device=dev), torch.randn(n, k, device=dev) * 0.02
@@ -42,9 +42,11 @@ def run(name, kind, m, n, k, epi, reps=10):
     else:
         a, b = torch.randn(k, m, device=dev), torch.randn(k, n, device=dev) * 0.02
         at, bt = 1, 0
-    c = torch.zeros(m, n, device=dev)
+    a, b = a.to(dtype), b.to(dtype)
+    cdt = torch.float32 if kind == "tn" else dtype   # weight gradients accumulate into fp32
+    c = torch.zeros(m, n, device=dev, dtype=cdt)
     bias = torch.zeros(n, device=dev)
-    aux = torch.randn(m, n, device=dev) if epi in (L.EPI_BIAS_GELU, L.EPI_DGELU) else None
+    aux = torch.randn(m, n, device=dev, dtype=cdt) if epi in (L.EPI_BIAS_GELU, L.EPI_DGELU) else None
     beta = 1.0 if kind == "tn" else 0.0
     s = ops._splitk(m, n, k) if kind == "tn" else 1
     ws = torch.empty(s * m * n, device=dev) if s > 1 else None
@@ -63,14 +65,18 @@ def run(name, kind, m, n, k, epi, reps=10):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
     tf = 2.0 * m * n * k / (ms * 1e-3) / 1e12
-    print("%-20s %s m=%6d n=%5d k=%6d splitk=%2d  %8.3f ms  %6.1f TF/s" % (name, kind, m, n, k, s, ms, tf), flush=True)
+    print("%-20s %s %s m=%6d n=%5d k=%6d splitk=%2d  %8.3f ms  %7.1f TF/s" % (name, kind, str(dtype)[6:], m, n, k, s,
+                                                                            ms, tf), flush=True)
     return tf
 
 
 if __name__ == "__main__":
     L.load()
-    only = sys.argv[1] if len(sys.argv) > 1 else None
+    only = sys.argv[1] if len(sys.argv) > 1 and sys.argv[1] != "all" else None
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-    for sh in SHAPES:
-        if only is None or sh[0] == only:
-            run(*sh, reps=reps)
+    dts = {"fp32": [torch.float32], "bf16": [torch.bfloat16], "both": [torch.float32, torch.bfloat16]}[
+        sys.argv[3] if len(sys.argv) > 3 else "fp32"]
+    for d in dts:
+        for sh in SHAPES:
+            if only is None or sh[0] == only:
+                run(*sh, reps=reps, dtype=d)

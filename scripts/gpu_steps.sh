@@ -25,7 +25,9 @@ for s in "$@"; do
     bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
     benchq) step bench 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     prof) export TMPDIR=/tmp; step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
-    gemm) step gemm 300 python scripts/gemm_bench.py ;;
+    gemm) step gemm 300 python scripts/gemm_bench.py all 10 both ;;
+    gemmbf) step gemmbf 300 python scripts/gemm_bench.py all 10 bf16 ;;
+    tbf) step tbf 600 python -m pytest tests/test_gpu_gemm_bf16.py -q ;;
     ddp2) step ddp2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --backend gloo --batch 16 ;;
     pmc) export TMPDIR=/tmp
          step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python scripts/gemm_bench.py "fwd ffn1 gelu" 5

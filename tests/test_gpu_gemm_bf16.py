@@ -1,0 +1,171 @@
+"""bf16-operand MFMA GEMM (gemm_bf16.hip) against a plain PyTorch fp32 reference of the same op
+on the bf16-rounded operands.  Accumulation is fp32 in both, so the fp32-C results agree to
+summation-order rounding (rel 1e-5 of max|ref| x sqrt(k) headroom); bf16-C results additionally
+carry one bf16 output rounding (rel 2^-8)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from k3m_amd import _lib
+    _lib.load()
+    return torch.device("cuda")
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-12))
+
+
+def _ops(m, n, k, at, bt, dev, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    A = torch.randn(m, k, generator=g).to(dev).bfloat16()
+    Bm = torch.randn(k, n, generator=g).to(dev).bfloat16()
+    a = A.t().contiguous() if at else A
+    b = Bm.t().contiguous() if bt else Bm
+    return A, Bm, a, b
+
+
+@pytest.mark.parametrize("m,n,k", [(128, 128, 64), (300, 200, 100), (2368, 1024, 2048), (37, 1601, 1024),
+                                   (64, 768, 5), (1000, 3072, 768), (20992 // 8, 768, 3072)])
+@pytest.mark.parametrize("at,bt", [(0, 1), (0, 0), (1, 0), (1, 1)])
+def test_gemm_bf16_layouts_f32c(dev, m, n, k, at, bt):
+    from k3m_amd import ops
+    A, Bm, a, b = _ops(m, n, k, at, bt, dev, m * 7 + n + k)
+    c = torch.randn(m, n, device=dev)
+    ref = 0.5 * (A.float() @ Bm.float()) + 0.25 * c
+    ops.gemm(a, at, b, bt, c, m, n, k, alpha=0.5, beta=0.25)
+    assert _rel(c, ref) < 1e-5
+
+
+@pytest.mark.parametrize("m,n,k", [(300, 200, 100), (1000, 3072, 768), (37, 1601, 1024)])
+@pytest.mark.parametrize("at,bt", [(0, 1), (0, 0)])
+def test_gemm_bf16_layouts_bf16c(dev, m, n, k, at, bt):
+    from k3m_amd import ops
+    A, Bm, a, b = _ops(m, n, k, at, bt, dev, m + n * 3 + k)
+    c = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+    ref = A.float() @ Bm.float()
+    ops.gemm(a, at, b, bt, c, m, n, k)
+    # one round-to-nearest of the fp32 sum: |err| <= 2^-9 |ref| elementwise
+    err = (c.float() - ref).abs()
+    assert bool((err <= ref.abs() * 2.0 ** -8 + 1e-6 * ref.abs().max()).all())
+
+
+@pytest.mark.parametrize("splitk", [2, 5])
+def test_gemm_bf16_splitk(dev, splitk):
+    from k3m_amd import ops
+    m, n, k = 768, 768, 20000
+    A = torch.randn(k, m, device=dev).bfloat16()
+    Bm = torch.randn(k, n, device=dev).bfloat16()
+    c = torch.randn(m, n, device=dev)
+    ref = A.float().t() @ Bm.float() + c
+    ws = torch.empty(splitk * m * n, device=dev)
+    ops.gemm(A, 1, Bm, 0, c, m, n, k, beta=1.0, splitk=splitk, ws=ws)
+    assert _rel(c, ref) < 1e-5
+
+
+def test_gemm_bf16_epilogues(dev):
+    from k3m_amd import ops, _lib as L
+    F = torch.nn.functional
+    x = torch.randn(500, 768, device=dev).bfloat16()
+    W = (torch.randn(3072, 768, device=dev) * 0.05).bfloat16()
+    b = torch.randn(3072, device=dev)
+    r = x.float() @ W.float().t() + b
+    pre = torch.empty(500, 3072, device=dev, dtype=torch.bfloat16)
+    y = torch.empty(500, 3072, device=dev, dtype=torch.bfloat16)
+    ops.gemm(x, 0, W, 1, y, 500, 3072, 768, L.EPI_BIAS_GELU, b, pre)
+    assert _rel(pre, r) < 2.0 ** -8
+    assert _rel(y, F.gelu(pre.float())) < 2.0 ** -8
+    s = torch.empty(500, 3072, device=dev)
+    ops.gemm(x, 0, W, 1, s, 500, 3072, 768, L.EPI_BIAS_SIGMOID, b)
+    assert _rel(s, torch.sigmoid(r)) < 1e-5
+    dy = torch.randn(500, 3072, device=dev).bfloat16()
+    pre2 = torch.randn(500, 768, device=dev).bfloat16()
+    dx = torch.empty(500, 768, device=dev, dtype=torch.bfloat16)
+    ops.gemm(dy, 0, W, 0, dx, 500, 768, 3072, L.EPI_DGELU, None, pre2)
+    xr = pre2.float().requires_grad_(True)
+    F.gelu(xr).backward(dy.float() @ W.float())
+    assert _rel(dx, xr.grad) < 2.0 ** -7
+
+
+# ---------------------------------------------------------------- bf16 storage in the other kernels
+def _ln_ref(s, g, b):
+    u = s.mean(-1, keepdim=True)
+    v = (s - u).pow(2).mean(-1, keepdim=True)
+    return g * (s - u) / torch.sqrt(v + 1e-12) + b
+
+
+@pytest.mark.parametrize("cols", [768, 1024])
+def test_layernorm_bf16(dev, cols):
+    """bf16 activations in/out, fp32 statistics and parameter gradients; reference = fp32 math on
+    the bf16 inputs; tolerance = bf16 output rounding."""
+    from k3m_amd import ops
+    M = 999
+    x = torch.randn(M, cols, device=dev).bfloat16()
+    r = torch.randn(M, cols, device=dev).bfloat16()
+    g = 1 + 0.1 * torch.randn(cols, device=dev)
+    b = 0.1 * torch.randn(cols, device=dev)
+    y = torch.empty_like(x)
+    xh = torch.empty_like(x)
+    rs = torch.empty(M, device=dev)
+    ops.ln_fwd(x, r, g, b, y, xh, rs)
+    xr, rr = x.float().requires_grad_(True), r.float().requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = _ln_ref(xr + rr, gr, br)
+    assert _rel(y, yr) < 2.0 ** -7
+    dy = torch.randn(M, cols, device=dev).bfloat16()
+    yr.backward(dy.float())
+    dres = torch.empty_like(x)
+    dg = torch.zeros(cols, device=dev)
+    db = torch.zeros(cols, device=dev)
+    ops.ln_bwd(dy, xh, rs, g, dres, dres, dg, db)
+    assert _rel(dres, xr.grad) < 2.0 ** -6
+    assert _rel(dg, gr.grad) < 1e-2
+    assert _rel(db, br.grad) < 1e-4
+
+
+def test_colsum_bf16(dev):
+    from k3m_amd import ops
+    x = torch.randn(20992, 768, device=dev).bfloat16()
+    out = torch.randn(768, device=dev)
+    ref = out + x.float().sum(0)
+    ops.colsum(x, out, accumulate=True)
+    assert _rel(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("lq,lk,nh,hd", [(36, 36, 12, 64), (128, 128, 12, 64), (37, 37, 8, 128), (36, 37, 8, 128),
+                                         (128, 36, 8, 96)])
+def test_attention_bf16(dev, lq, lk, nh, hd):
+    """bf16 q/k/v/ctx (fp32 softmax and probabilities) against fp32 math on the same bf16 inputs."""
+    import math
+    from k3m_amd import ops
+    B, D = 5, nh * hd
+    qkv_q = torch.randn(B * lq, 3 * D, device=dev).bfloat16()
+    qkv_k = torch.randn(B * lk, 3 * D, device=dev).bfloat16()
+    q, k, v = qkv_q[:, :D], qkv_k[:, D:2 * D], qkv_k[:, 2 * D:]
+    m = torch.ones(B, lk, device=dev)
+    m[:, lk - 3:] = 0
+    mask = ((1 - m) * -10000).contiguous()
+    ctx = torch.empty(B * lq, D, device=dev, dtype=torch.bfloat16)
+    probs = torch.empty(B * nh * lq * lk, device=dev)
+    ops.attn_fwd(q, k, v, mask, ctx, probs, B, lq, lk, nh, hd, 1 / math.sqrt(hd), 0.0, 0, 0)
+    qr, kr, vr = [t.float().reshape(B, -1, D).clone().requires_grad_(True) for t in (q, k, v)]
+    qh = qr.view(B, lq, nh, hd).permute(0, 2, 1, 3)
+    kh = kr.view(B, lk, nh, hd).permute(0, 2, 1, 3)
+    vh = vr.view(B, lk, nh, hd).permute(0, 2, 1, 3)
+    p = torch.softmax(qh @ kh.transpose(-1, -2) / math.sqrt(hd) + mask[:, None, None, :], -1)
+    cr = (p @ vh).permute(0, 2, 1, 3).reshape(B, lq, D)
+    assert _rel(probs.view(B, nh, lq, lk), p) < 1e-4
+    assert _rel(ctx.view(B, lq, D), cr) < 2.0 ** -7
+    dctx = torch.randn(B * lq, D, device=dev).bfloat16()
+    cr.backward(dctx.float().view(B, lq, D))
+    dq, dk, dv = [torch.empty(B * n_, D, device=dev, dtype=torch.bfloat16) for n_ in (lq, lk, lk)]
+    ops.attn_bwd(dctx, ctx, q, k, v, probs, dq, dk, dv, B, lq, lk, nh, hd, 1 / math.sqrt(hd), 0.0, 0, 0)
+    # dS uses the bf16-rounded ctx in D = rowdot(dO, O): a few bf16 ulps of slack
+    assert _rel(dq.view(B, lq, D), qr.grad) < 2e-2
+    assert _rel(dk.view(B, lk, D), kr.grad) < 2e-2
+    assert _rel(dv.view(B, lk, D), vr.grad) < 2.0 ** -6
