@@ -35,6 +35,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="fp32: configs[1] (the metric's config); bf16: mixed-precision encoder (configs[2])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=2)
     ap.add_argument("--cpu-steps", type=int, default=3)
@@ -150,7 +152,7 @@ def main():
     cfg = pretrain_config(os.path.join(HERE, "configs", "bert_base_6layer_6conect.json"))
     B = args.batch
     tr = Trainer(cfg, dev, lr=1e-4, warmup_steps=max(1, (args.steps + args.warmup) // 10),
-                 total_steps=10 * (args.steps + args.warmup), seed=1234, init=True)
+                 total_steps=10 * (args.steps + args.warmup), seed=1234, init=True, dtype=args.dtype)
     if world > 1:
         ddp = GradAllReducer(tr.engine.fp)
         ddp.broadcast_params(tr.engine.fp)
@@ -188,24 +190,28 @@ def main():
     Mg, Ng, Kg = probe.key
     gemm_flops = 2.0 * Mg * Ng * Kg
     achieved = gemm_flops / (gemm_ms * 1e-3) if gemm_ms else None
+    bf = args.dtype == "bf16"
+    peak = PEAK_BF16_MFMA if bf else PEAK_F32_MFMA
+    kname = "gemm_bf16_kernel" if bf else "gemm_f32_kernel"
     res = {
         "metric": "pretrain samples/sec (whole job; bert_base_6layer_6conect, bs=64/GPU)",
         "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "fp32", "data": "synthetic (SURVEY §8(d): random token ids, 36x2048 region feats, 10 PV triples)",
-        "config": {"workload": "config 2: bert_base_6layer_6conect fp32 bs=64/GPU T=36 P=128 R=37 10 triples",
+        "dtype": args.dtype, "data": "synthetic (SURVEY §8(d): random token ids, 36x2048 region feats, 10 PV triples)",
+        "config": {"workload": "config %d: bert_base_6layer_6conect %s bs=%d/GPU T=36 P=128 R=37 10 triples" % (
+                       3 if bf else 2, "bf16 encoder (fp32 master weights, heads, AdamW)" if bf else "fp32", B),
                    "model": "bert_base_6layer_6conect", "global_batch": B * world, "seq_len": T,
                    "parallelism": "dp%d" % world},
         "per_gpu_samples_s": round(value / world, 3),
         "loss": round(loss, 4),
-        "step_mfma_frac_vs_ref_flops": round(B * REF_FLOPS_PER_SAMPLE / (ms_step * 1e-3) / PEAK_F32_MFMA, 4),
-        "roofline": {"bound": "mfma", "kernel": "gemm_f32 text-layer FFN1 %dx%dx%d" % (Mg, Ng, Kg),
+        "step_mfma_frac_vs_ref_flops": round(B * REF_FLOPS_PER_SAMPLE / (ms_step * 1e-3) / peak, 4),
+        "roofline": {"bound": "mfma", "kernel": "%s text-layer FFN1 %dx%dx%d" % (kname, Mg, Ng, Kg),
                      "achieved": round(achieved / 1e12, 2) if achieved else None,
-                     "peak": PEAK_F32_MFMA / 1e12, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_F32_MFMA, 4) if achieved else None,
+                     "peak": peak / 1e12, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4) if achieved else None,
                      "avg_launch_ms": round(gemm_ms, 4) if gemm_ms else None,
                      "launches": len(probe.events),
-                     "traffic": pmc_traffic(probe.key, "void (anonymous namespace)::gemm_f32_kernel"),
+                     "traffic": pmc_traffic(probe.key, "void (anonymous namespace)::" + kname),
                      "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/r1_gemm_ffn1_pmc.json)"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -208,6 +208,11 @@ int k3m_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, lo
 
 /* Cast helpers for the mixed-precision path. */
 int k3m_cast_f32_bf16(const float* x, uint16_t* y, long long n, hipStream_t stream);
+/* y = (accumulate ? y : 0) + alpha * x with a type conversion (fp32 <-> bf16): the boundary between
+ * the fp32 heads/fusion and a bf16 encoder, and the bf16 weight shadow.  (Mixed-precision
+ * plumbing; the reference's fp16 path is apex amp, train_concap_struc.py:409-432.) */
+int k3m_convert(const void* x, int xdtype, void* y, int ydtype, long long n, int accumulate, float alpha,
+                hipStream_t stream);
 int k3m_add_inplace(void* y, const void* x, long long n, float alpha, int dtype, hipStream_t stream);
 
 #ifdef __cplusplus

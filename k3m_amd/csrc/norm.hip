@@ -286,6 +286,13 @@ __global__ void cast_kernel(const float* x, uint16_t* y, long long n) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
     y[i] = from_f<bf16_t>(x[i]).x;
 }
+template <typename X, typename Y>
+__global__ void convert_kernel(const X* x, Y* y, long long n, int accumulate, float alpha) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float v = alpha * to_f(x[i]);
+    y[i] = from_f<Y>(accumulate ? to_f(y[i]) + v : v);
+  }
+}
 template <typename T>
 __global__ void gather_rows_kernel(const T* src, long long lds, const int32_t* idx, int n, int cols, T* dst,
                                    long long ldd) {
@@ -409,6 +416,28 @@ extern "C" int k3m_cast_f32_bf16(const float* x, uint16_t* y, long long n, hipSt
   K3M_ARG(x && y);
   if (n == 0) return 0;
   hipLaunchKernelGGL(cast_kernel, dim3(grid_for(n)), dim3(256), 0, st, x, y, n);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_convert(const void* x, int xdtype, void* y, int ydtype, long long n, int accumulate, float alpha,
+                           hipStream_t st) {
+  K3M_ARG(x && y && n >= 0);
+  if (n == 0) return 0;
+  if (xdtype == K3M_F32 && ydtype == K3M_BF16)
+    hipLaunchKernelGGL((convert_kernel<float, bf16_t>), dim3(grid_for(n)), dim3(256), 0, st, (const float*)x,
+                       (bf16_t*)y, n, accumulate, alpha);
+  else if (xdtype == K3M_BF16 && ydtype == K3M_F32)
+    hipLaunchKernelGGL((convert_kernel<bf16_t, float>), dim3(grid_for(n)), dim3(256), 0, st, (const bf16_t*)x,
+                       (float*)y, n, accumulate, alpha);
+  else if (xdtype == K3M_F32 && ydtype == K3M_F32)
+    hipLaunchKernelGGL((convert_kernel<float, float>), dim3(grid_for(n)), dim3(256), 0, st, (const float*)x,
+                       (float*)y, n, accumulate, alpha);
+  else if (xdtype == K3M_BF16 && ydtype == K3M_BF16)
+    hipLaunchKernelGGL((convert_kernel<bf16_t, bf16_t>), dim3(grid_for(n)), dim3(256), 0, st, (const bf16_t*)x,
+                       (bf16_t*)y, n, accumulate, alpha);
+  else
+    return K3M_EINVAL;
   K3M_CHECK_LAUNCH();
   return 0;
 }

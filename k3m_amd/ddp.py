@@ -71,6 +71,7 @@ class GradAllReducer(object):
 
     def broadcast_params(self, fp):
         dist.broadcast(fp.data, src=0, group=self.group)
+        fp.shadow_fresh = False
 
     def begin(self, engine):
         self.done = set()

@@ -49,13 +49,17 @@ class Rng(object):
 
 
 class FlatParams(object):
-    """All parameters (and their gradients) as views into single contiguous fp32 buffers."""
+    """All parameters (and their gradients) as views into single contiguous fp32 buffers, plus an
+    optional bf16 shadow of the parameters (the operand copy for a bf16 encoder; fp32 stays the
+    master copy that AdamW updates)."""
 
-    def __init__(self, cfg, device):
+    def __init__(self, cfg, device, bf16_shadow=False):
         self.spec, self.offsets, self.segments, self.total, self.shapes = flat_layout(cfg)
         self.device = device
         self.data = torch.zeros(self.total, dtype=torch.float32, device=device)
         self.grad = torch.zeros(self.total, dtype=torch.float32, device=device)
+        self.data16 = torch.zeros(self.total, dtype=torch.bfloat16, device=device) if bf16_shadow else None
+        self.shadow_fresh = False
         self.p, self.g = {}, {}
         for name, shape in self.spec:
             o = self.offsets[name]
@@ -63,9 +67,9 @@ class FlatParams(object):
             self.p[name] = self.data[o:o + n].view(shape)
             self.g[name] = self.grad[o:o + n].view(shape)
 
-    def fused(self, names, grad=False):
+    def fused(self, names, grad=False, bf16=False):
         """Contiguous view spanning adjacent tensors (e.g. query|key|value weights -> [3H, H])."""
-        buf = self.grad if grad else self.data
+        buf = self.grad if grad else (self.data16 if bf16 else self.data)
         o = self.offsets[names[0]]
         n = 0
         for nm in names:
@@ -80,6 +84,14 @@ class FlatParams(object):
             v = values[name]
             t = torch.as_tensor(v) if not isinstance(v, torch.Tensor) else v
             self.p[name].copy_(t.to(torch.float32).reshape(self.shapes[name]))
+        self.shadow_fresh = False
+
+    def refresh_shadow(self):
+        """bf16 shadow <- fp32 parameters (after loads / external optimizers; the Trainer's AdamW
+        writes the shadow itself)."""
+        if self.data16 is not None and not self.shadow_fresh:
+            ops.convert(self.data, self.data16)
+        self.shadow_fresh = True
 
     def state_dict(self):
         sd = {}
@@ -99,15 +111,20 @@ class Lin(object):
         b = [p + ".bias" for p in prefixes]
         self.W, self.gW = fp.fused(w), fp.fused(w, True)
         self.b, self.gb = fp.fused(b), fp.fused(b, True)
+        self.W16 = fp.fused(w, bf16=True) if fp.data16 is not None else None
+
+    def _w(self, x):
+        # operands share a dtype: a bf16 activation multiplies the bf16 weight shadow
+        return self.W16 if x.dtype == torch.bfloat16 else self.W
 
     def fwd(self, x, out=None, epi=None, aux=None, alpha=1.0, beta=0.0):
-        return ops.linear(x, self.W, self.b, out=out, epi=epi, aux=aux, alpha=alpha, beta=beta)
+        return ops.linear(x, self._w(x), self.b, out=out, epi=epi, aux=aux, alpha=alpha, beta=beta)
 
     def wgrad(self, dy, x, alpha=1.0):
         ops.linear_wgrad(dy, x, self.gW, self.gb, alpha=alpha)
 
     def dgrad(self, dy, dx=None, beta=0.0, dgelu_aux=None, alpha=1.0):
-        return ops.linear_dgrad(dy, self.W, dx=dx, beta=beta, dgelu_aux=dgelu_aux, alpha=alpha)
+        return ops.linear_dgrad(dy, self._w(dy), dx=dx, beta=beta, dgelu_aux=dgelu_aux, alpha=alpha)
 
 
 class LN(object):
@@ -287,11 +304,18 @@ def _ext_mask(m):
 class K3MEngine(object):
     """One replica of the model on one GPU (one process per GPU; DDP in k3m_amd/ddp.py)."""
 
-    def __init__(self, cfg, device=None, seed=1234):
+    def __init__(self, cfg, device=None, seed=1234, dtype="fp32"):
+        """dtype: "fp32" (everything fp32) or "bf16" (mixed precision: the encoder — text, image and
+        co-attention layers, >95% of the FLOPs — keeps activations and activation gradients in bf16
+        and multiplies the bf16 weight shadow on the bf16 MFMA; embeddings, fusion, heads, losses,
+        parameter gradients and AdamW stay fp32)."""
         self.cfg = cfg
         self.device = torch.device(device if device is not None else "cuda")
         L.load()
-        fp = self.fp = FlatParams(cfg, self.device)
+        assert dtype in ("fp32", "bf16")
+        self.dtype = dtype
+        self.enc_dtype = torch.bfloat16 if dtype == "bf16" else torch.float32
+        fp = self.fp = FlatParams(cfg, self.device, bf16_shadow=(dtype == "bf16"))
         self.base_seed = int(seed)
         self.step_count = 0
         c = cfg
@@ -356,8 +380,10 @@ class K3MEngine(object):
         noise: optional {v,t,pv: [B, L, 3, D]} gumbel noise; ent_neg/val_neg optional [B,NPV,2]."""
         c = self.cfg
         fp = self.fp
+        fp.refresh_shadow()
         dev = self.device
         H, Hv = self.H, self.Hv
+        ED = self.enc_dtype
         ids, tt, mt = batch["input_ids"], batch["segment_ids"], batch["input_mask"]
         pids, ptt, mp = batch["input_ids_pv"], batch["segment_ids_pv"], batch["input_mask_pv"]
         feat, loc, mv = batch["image_feat"], batch["image_loc"], batch["image_mask"]
@@ -403,9 +429,11 @@ class K3MEngine(object):
         rs_v = torch.empty((BR,), dtype=torch.float32, device=dev)
         off_v = rng.take(BR * Hv) if ph > 0 else 0
         ops.ln_fwd(img, lce, self.vemb_ln.g, self.vemb_ln.b, ind_v, xh_v, rs_v, p_out=ph, seed=rng.seed, off_out=off_v)
-        XV = torch.empty((2 * BR, Hv), dtype=torch.float32, device=dev)
-        XV[0:BR].copy_(ind_v)
-        XV[BR:].copy_(ind_v)
+        XV = torch.empty((2 * BR, Hv), dtype=ED, device=dev)
+        ops.convert(ind_v, XV[0:BR])
+        ops.convert(ind_v, XV[BR:])
+        if ED != torch.float32:
+            XT = ops.convert(XT, torch.empty((Nt, H), dtype=ED, device=dev))
         ctx["vemb"] = (feat2, loc2, xh_v, rs_v, off_v)
 
         # ---- encoder, lock-step wide passes
@@ -439,6 +467,9 @@ class K3MEngine(object):
                 enc.append((kind, i, (s_tv, s_pv, s_tt, ops_)))
                 XT, XV = XT2, XV2
         ctx["enc"] = enc
+        if ED != torch.float32:   # encoder -> fp32 fusion / heads
+            XT = ops.convert(XT, torch.empty((Nt, H), dtype=torch.float32, device=dev))
+            XV = ops.convert(XV, torch.empty((2 * BR, Hv), dtype=torch.float32, device=dev))
         ctx["XT"], ctx["XV"] = XT, XV
 
         # ---- initial-interactive fusion (get_sequence_pooled_output_final :2376-2411)
@@ -718,6 +749,9 @@ class K3MEngine(object):
             d_ind[m] = d0
 
         # ---- encoder (reverse lock-step)
+        if self.enc_dtype != torch.float32:
+            dXT = ops.convert(dXT, torch.empty(dXT.shape, dtype=self.enc_dtype, device=dev))
+            dXV = ops.convert(dXV, torch.empty(dXV.shape, dtype=self.enc_dtype, device=dev))
         for kind, i, sv in reversed(ctx["enc"]):
             if kind == "t":
                 op = self.text[i] if ctx["train"] else _eval_view(self.text[i])
@@ -739,14 +773,14 @@ class K3MEngine(object):
         # ---- embeddings
         ph = self.p_h if ctx["train"] else 0.0
         dt_ = d_ind["t"]
-        ops.add_(dt_, dXT[0:BT].contiguous())
-        ops.add_(dt_, dXT[BT:2 * BT].contiguous())
+        ops.convert(dXT[0:BT], dt_, accumulate=True)
+        ops.convert(dXT[BT:2 * BT], dt_, accumulate=True)
         dp_ = d_ind["pv"]
-        ops.add_(dp_, dXT[2 * BT:2 * BT + BP].contiguous())
-        ops.add_(dp_, dXT[2 * BT + BP:].contiguous())
+        ops.convert(dXT[2 * BT:2 * BT + BP], dp_, accumulate=True)
+        ops.convert(dXT[2 * BT + BP:], dp_, accumulate=True)
         dv_ = d_ind["v"]
-        ops.add_(dv_, dXV[0:BR].contiguous())
-        ops.add_(dv_, dXV[BR:].contiguous())
+        ops.convert(dXV[0:BR], dv_, accumulate=True)
+        ops.convert(dXV[BR:], dv_, accumulate=True)
         xh_t, rs_t, off_t, xh_p, rs_p, off_p = ctx["emb"]
         gword = fp.g["embeddings.word_embeddings.weight"]
         gpos = fp.g["embeddings.position_embeddings.weight"]

@@ -145,6 +145,13 @@ def add_(y, x, alpha=1.0):
     call("k3m_add_inplace", ptr(y), ptr(x), y.numel(), alpha, dt(y), stream())
 
 
+def convert(x, y, accumulate=False, alpha=1.0):
+    """y (+)= alpha * x across dtypes (fp32 <-> bf16); both contiguous with equal numel."""
+    assert x.numel() == y.numel() and x.is_contiguous() and y.is_contiguous()
+    call("k3m_convert", ptr(x), dt(x), ptr(y), dt(y), x.numel(), int(accumulate), alpha, stream())
+    return y
+
+
 def gather_rows(src, idx, n, out):
     call("k3m_gather_rows", ptr(src), _ld(src), ptr(idx), n, src.shape[1], ptr(out), _ld(out), dt(src), stream())
 

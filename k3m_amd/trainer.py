@@ -34,12 +34,13 @@ def init_reference(fp, cfg, seed):
             t.zero_()
         else:
             t.normal_(0.0, std, generator=g)
+    fp.shadow_fresh = False
 
 
 class Trainer(object):
     def __init__(self, cfg, device, lr=1e-4, warmup_steps=0, total_steps=10000, seed=1234, ddp=None,
-                 loss_img_weight=1.0, beta1=0.9, beta2=0.98, eps=1e-8, weight_decay=0.01, init=True):
-        self.engine = K3MEngine(cfg, device, seed=seed)
+                 loss_img_weight=1.0, beta1=0.9, beta2=0.98, eps=1e-8, weight_decay=0.01, init=True, dtype="fp32"):
+        self.engine = K3MEngine(cfg, device, seed=seed, dtype=dtype)
         fp = self.engine.fp
         if init:
             init_reference(fp, cfg, seed)
@@ -66,12 +67,16 @@ class Trainer(object):
         fp = self.engine.fp
         lr = self.current_lr()
         step = self.global_step + 1
+        fresh = fp.shadow_fresh
         for off, n, wd in self.segs:
             if n == 0:
                 continue
+            # with a bf16 encoder the same launch refreshes the weight shadow from the new fp32 values
+            sh = fp.data16[off:].data_ptr() if fp.data16 is not None else None
             L.call("k3m_adamw", fp.data[off:].data_ptr(), fp.grad[off:].data_ptr(), self.m[off:].data_ptr(),
-                   self.v[off:].data_ptr(), None, n, lr, self.beta1, self.beta2, self.eps, wd, step, grad_scale,
+                   self.v[off:].data_ptr(), sh, n, lr, self.beta1, self.beta2, self.eps, wd, step, grad_scale,
                    L.stream())
+        fp.shadow_fresh = fresh   # frozen tensors are not updated: the shadow stays as fresh as it was
         fp.grad.zero_()
         self.global_step += 1
 

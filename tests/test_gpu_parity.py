@@ -21,13 +21,13 @@ def dev():
 _ENG = {}
 
 
-def engine_for(cfg, seed, dev):
+def engine_for(cfg, seed, dev, dtype="fp32"):
     from k3m_amd.engine import K3MEngine
     from k3m_amd.weights import param_values
-    key = (cfg.if_pre_sampling, seed)
+    key = (cfg.if_pre_sampling, seed, dtype)
     if key not in _ENG:
         _ENG.clear()
-        e = K3MEngine(cfg, dev)
+        e = K3MEngine(cfg, dev, dtype=dtype)
         e.fp.load(param_values(cfg, seed))
         _ENG[key] = e
     e = _ENG[key]
@@ -80,6 +80,65 @@ def test_train_mode_step_is_finite_and_learns(dev):
     from golden_util import CFG_PATH
     cfg = pretrain_config(CFG_PATH)
     tr = Trainer(cfg, dev, lr=2e-4, warmup_steps=0, total_steps=100, seed=3)
+    batch = synthetic_batch(cfg, 8, dev, seed=5)
+    losses = []
+    for _ in range(6):
+        out = tr.step(batch)
+        losses.append(float(out["loss"]))
+    assert all(np.isfinite(losses)), losses
+    assert losses[-1] < losses[0], losses
+
+
+# ---------------------------------------------------------------- bf16 encoder (configs[2] precision)
+# The bf16 mode rounds encoder activations and weights to bf16 (8 significant bits), so it is
+# compared with the reference's fp32 golden values at mixed-precision tolerances: losses within
+# BF16_LOSS_RTOL, and every recorded gradient tensor with cosine similarity >= BF16_GRAD_COS and
+# norm within BF16_GRAD_NORM_RTOL of the fp32 reference.
+BF16_LOSS_RTOL = 1e-2
+BF16_GRAD_COS = 0.999
+BF16_GRAD_NORM_RTOL = 3e-2
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_bf16_engine_close_to_reference_golden(dev, case):
+    g = load_case(case)
+    cfg = case_config(g)
+    eng = engine_for(cfg, int(g["weight_seed"]), dev, dtype="bf16")
+    batch = {k: v.to(dev) for k, v in case_batch(g).items()}
+    noise = {k: v.to(dev) for k, v in case_noise(g).items()}
+    out, ctx = eng.forward(batch, train=False, noise=noise, ent_neg=torch.from_numpy(g["ent_neg"]),
+                           val_neg=torch.from_numpy(g["val_neg"]))
+    eng.backward(ctx)
+    torch.cuda.synchronize()
+    got = np.array([float(out[k]) for k in ("masked_lm_loss", "masked_img_loss", "masked_lm_loss_pv", "loss_lpm",
+                                           "next_sentence_loss", "loss")])
+    rel = np.abs(got - g["losses"]) / np.maximum(np.abs(g["losses"]), 1e-3)
+    print("bf16 loss rel err", case, rel)
+    assert (rel <= BF16_LOSS_RTOL).all(), (got, g["losses"])
+    G = eng.fp.g
+    worst_cos, worst_norm = 1.0, 0.0
+    for k in g:
+        if k.startswith("grad_full/"):
+            n = k.split("/", 1)[1]
+            a = G[n].double().cpu().numpy().ravel()
+            b = g[k].astype(np.float64).ravel()
+            nb = np.linalg.norm(b)
+            if nb < 1e-6:
+                continue
+            cos = float(a @ b / (np.linalg.norm(a) * nb + 1e-30))
+            nr = abs(np.linalg.norm(a) - nb) / nb
+            worst_cos, worst_norm = min(worst_cos, cos), max(worst_norm, nr)
+            assert cos >= BF16_GRAD_COS and nr <= BF16_GRAD_NORM_RTOL, (n, cos, nr)
+    print("bf16 grads: worst cos %.5f worst norm rel %.4f" % (worst_cos, worst_norm))
+
+
+def test_bf16_train_mode_learns(dev):
+    from k3m_amd.config import pretrain_config
+    from k3m_amd.trainer import Trainer
+    from k3m_amd.synthetic import synthetic_batch
+    from golden_util import CFG_PATH
+    cfg = pretrain_config(CFG_PATH)
+    tr = Trainer(cfg, dev, lr=2e-4, warmup_steps=0, total_steps=100, seed=3, dtype="bf16")
     batch = synthetic_batch(cfg, 8, dev, seed=5)
     losses = []
     for _ in range(6):
