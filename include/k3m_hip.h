@@ -75,9 +75,12 @@ int k3m_ln_fwd(const void* x, const void* res, const float* gamma, const float* 
                uint64_t off_in, uint64_t off_out, int dtype, hipStream_t stream);
 /* Backward of k3m_ln_fwd.  ds = d(pre-LN sum) is written to dres (or accumulated when
  * accumulate_res), dx = dropout_in'(ds) is written to dx (may alias dres when p_in == 0).
- * dgamma/dbeta are ACCUMULATED (fp32 grad buffer).  ws: >= 2*128*cols floats. */
+ * dgamma/dbeta are ACCUMULATED (fp32 grad buffer).  dxsum (nullable): the column sums of dx are
+ * ACCUMULATED into it — the bias gradient of the Linear that produced x, fused here instead of a
+ * separate reduction over dx.  ws: >= 3*K3M_LN_BWD_SLABS*cols floats. */
+#define K3M_LN_BWD_SLABS 512
 int k3m_ln_bwd(const void* dy, const void* xhat, const float* rstd, const float* gamma, void* dres, void* dx,
-               float* dgamma, float* dbeta, int rows, int cols, float p_in, float p_out, uint64_t seed,
+               float* dgamma, float* dbeta, float* dxsum, int rows, int cols, float p_in, float p_out, uint64_t seed,
                uint64_t off_in, uint64_t off_out, int accumulate_res, float* ws, int dtype, hipStream_t stream);
 
 /* BertEmbeddings (vilbert_k3m.py:361-382): word + position + token-type -> LN -> dropout.
@@ -106,6 +109,19 @@ int k3m_attn_bwd(const void* dctx, long long ldc, const void* o, long long ldo, 
                  const void* k, long long ldk, const void* v, long long ldv, const float* probs, void* dq, void* dk,
                  void* dv, long long lddq, long long lddk, long long lddv, int nseq, int lq, int lk, int nh, int hd,
                  float scale, float p_drop, uint64_t seed, uint64_t off, int dtype, hipStream_t stream);
+
+/* bf16 attention for the mixed-precision encoder (same semantics as k3m_attn_fwd/bwd; head dim
+ * 64 or 128, L <= 128): instead of the [nseq, nh, lq, lk] probabilities the forward saves the row
+ * log-sum-exp lse [nseq, nh, lq] and the backward recomputes P from it (kmask is needed again).
+ * Every row pointer + ld must allow 16-byte loads (ld % 8 == 0, 16-B aligned base). */
+int k3m_flash_attn_fwd(const void* q, long long ldq, const void* k, long long ldk, const void* v, long long ldv,
+                       const float* kmask, void* ctx, long long ldc, float* lse, int nseq, int lq, int lk, int nh,
+                       int hd, float scale, float p_drop, uint64_t seed, uint64_t off, hipStream_t stream);
+int k3m_flash_attn_bwd(const void* dctx, long long ldc, const void* o, long long ldo, const void* q, long long ldq,
+                       const void* k, long long ldk, const void* v, long long ldv, const float* kmask,
+                       const float* lse, void* dq, void* dk, void* dv, long long lddq, long long lddk, long long lddv,
+                       int nseq, int lq, int lk, int nh, int hd, float scale, float p_drop, uint64_t seed,
+                       uint64_t off, hipStream_t stream);
 
 /* Elementwise: out = g * gelu'(pre) (backward of the MLM/image head transforms :1795-1818). */
 int k3m_dgelu(const void* g, const void* pre, void* out, long long n, int dtype, hipStream_t stream);

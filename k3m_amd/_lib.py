@@ -31,12 +31,16 @@ SIGNATURES = {
     "k3m_gemm": [C.POINTER(K3mGemm), vp],
     "k3m_colsum": [vp, i64, i32, i32, vp, i32, vp, i32, vp],
     "k3m_ln_fwd": [vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, f32, u64, u64, u64, i32, vp],
-    "k3m_ln_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, u64, u64, u64, i32, vp, i32, vp],
+    "k3m_ln_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, u64, u64, u64, i32, vp, i32, vp],
     "k3m_embed_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, u64, u64, i32, vp],
     "k3m_embed_bwd": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp],
     "k3m_attn_fwd": [vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, i32, f32, f32, u64, u64, i32, vp],
     "k3m_attn_bwd": [vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, vp, vp, vp, i64, i64, i64, i32, i32, i32, i32,
                      i32, f32, f32, u64, u64, i32, vp],
+    "k3m_flash_attn_fwd": [vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, i32, f32, f32, u64, u64,
+                           vp],
+    "k3m_flash_attn_bwd": [vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, vp, vp, vp, vp, i64, i64, i64, i32, i32,
+                           i32, i32, i32, f32, f32, u64, u64, vp],
     "k3m_dgelu": [vp, vp, vp, i64, i32, vp],
     "k3m_gather_rows": [vp, i64, vp, i32, i32, vp, i64, i32, vp],
     "k3m_scatter_add_rows": [vp, i64, vp, i32, i32, vp, i64, i32, vp],

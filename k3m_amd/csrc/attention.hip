@@ -26,13 +26,63 @@ constexpr int NTH = NW * 64;
 
 __device__ __forceinline__ int sw(int i, int c, int cols) { return i * cols + (c ^ (i & 31)); }
 
+// Staging HBM -> LDS in two halves so the loads of the next operand can be issued before the
+// current phase's MFMAs and written after its barrier: every thread loads its 16-byte chunks
+// (8 bf16 / 4 fp32 of one row) into registers first — one HBM latency per operand, not one per
+// element — then converts and writes them into the swizzled fp32 image (rows >= nvalid are zero).
+template <typename T>
+struct Chunks {
+  static constexpr int VE = 16 / sizeof(T);
+  static constexpr int N = MAXL * MAXD / VE / NTH;  // chunks per thread for the largest tile
+  uint4 r[N];
+};
+
+template <typename T>
+__device__ __forceinline__ void stage_load(Chunks<T>& ch, const T* __restrict__ src, long long row0, long long ld,
+                                           int coff, int nrows, int nvalid, int cols) {
+  constexpr int VE = Chunks<T>::VE;
+  const int cpr = cols / VE, nch = nrows * cpr;
+#pragma unroll
+  for (int u = 0; u < Chunks<T>::N; ++u) {
+    const int e = threadIdx.x + u * NTH;
+    ch.r[u] = make_uint4(0u, 0u, 0u, 0u);
+    if (e < nch) {
+      const int i = e / cpr, c = (e - i * cpr) * VE;
+      if (i < nvalid) ch.r[u] = *reinterpret_cast<const uint4*>(src + (row0 + i) * ld + coff + c);
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void stage_store(float* __restrict__ dst, const Chunks<T>& ch, int nrows, int cols) {
+  constexpr int VE = Chunks<T>::VE;
+  const int cpr = cols / VE, nch = nrows * cpr;
+#pragma unroll
+  for (int u = 0; u < Chunks<T>::N; ++u) {
+    const int e = threadIdx.x + u * NTH;
+    if (e < nch) {
+      const int i = e / cpr, c = (e - i * cpr) * VE;
+      const uint32_t w4[4] = {ch.r[u].x, ch.r[u].y, ch.r[u].z, ch.r[u].w};
+      if constexpr (VE == 8) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          dst[sw(i, c + 2 * q, cols)] = __uint_as_float(w4[q] << 16);
+          dst[sw(i, c + 2 * q + 1, cols)] = __uint_as_float(w4[q] & 0xffff0000u);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dst[sw(i, c + q, cols)] = __uint_as_float(w4[q]);
+      }
+    }
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ void stage(float* __restrict__ dst, const T* __restrict__ src, long long row0, long long ld,
                                       int coff, int nrows, int nvalid, int cols) {
-  for (int e = threadIdx.x; e < nrows * cols; e += NTH) {
-    const int i = e / cols, c = e - (e / cols) * cols;
-    dst[sw(i, c, cols)] = i < nvalid ? to_f(src[(row0 + i) * ld + coff + c]) : 0.f;
-  }
+  Chunks<T> ch;
+  stage_load(ch, src, row0, ld, coff, nrows, nvalid, cols);
+  stage_store(dst, ch, nrows, cols);
 }
 
 // ------------------------------------------------------------------ forward
@@ -57,6 +107,8 @@ __global__ __launch_bounds__(NTH) void attn_fwd_kernel(const T* __restrict__ q, 
   stage(Qs, q, qrow0, ldq, hoff, LQ, lq, hd);
   stage(KVs, k, krow0, ldk, hoff, LK, lk, hd);
   __syncthreads();
+  Chunks<T> vch;  // V's loads fly while S is computed
+  stage_load(vch, v, krow0, ldv, hoff, LK, lk, hd);
   // S = scale * Q K^T + mask
   {
     const int tq = LQ >> 5, tk = LK >> 5;
@@ -80,7 +132,7 @@ __global__ __launch_bounds__(NTH) void attn_fwd_kernel(const T* __restrict__ q, 
     }
   }
   __syncthreads();
-  stage(KVs, v, krow0, ldv, hoff, LK, lk, hd);  // K no longer needed
+  stage_store(KVs, vch, LK, hd);  // K no longer needed
   // softmax rows (wave per row, lanes over keys), dropout, save P
   for (int i = w; i < LQ; i += NW) {
     const float x0 = lane < LK ? Ss[sw(i, lane, LK)] : -INFINITY;
@@ -165,14 +217,34 @@ __global__ __launch_bounds__(NTH) void attn_bwd_kernel(const T* __restrict__ dct
 
   stage(R1, dctx, qrow0, ldc, hoff, LQ, lq, hd);
   stage(R2, v, krow0, ldv, hoff, LK, lk, hd);
-  if (threadIdx.x < LQ) {
-    const int i = threadIdx.x;
-    float a = 0.f;
-    if (i < lq)
-      for (int d = 0; d < hd; ++d) a += to_f(dctx[(qrow0 + i) * ldc + hoff + d]) * to_f(o[(qrow0 + i) * ldo + hoff + d]);
-    Ds[i] = a;
+  // D_i = dO_i . O_i: a wave per row, lanes over the head dimension (all loads issued first)
+  {
+    constexpr int RW = MAXL / NW;   // rows per wave
+    float pa[RW][MAXD / 64], pb[RW][MAXD / 64];
+#pragma unroll
+    for (int u = 0; u < RW; ++u) {
+      const int i = w + u * NW;
+#pragma unroll
+      for (int c = 0; c < MAXD / 64; ++c) {
+        const int d = lane + 64 * c;
+        const bool ok = i < lq && d < hd;
+        pa[u][c] = ok ? to_f(dctx[(qrow0 + i) * ldc + hoff + d]) : 0.f;
+        pb[u][c] = ok ? to_f(o[(qrow0 + i) * ldo + hoff + d]) : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RW; ++u) {
+      float a = 0.f;
+#pragma unroll
+      for (int c = 0; c < MAXD / 64; ++c) a += pa[u][c] * pb[u][c];
+      a = wave_sum(a);
+      const int i = w + u * NW;
+      if (lane == 0 && i < LQ) Ds[i] = a;
+    }
   }
   __syncthreads();
+  Chunks<T> nch;  // K's loads fly during phase 1
+  stage_load(nch, k, krow0, ldk, hoff, LK, lk, hd);
   // phase 1: dS
   {
     const int tq = LQ >> 5, tk = LK >> 5;
@@ -200,8 +272,9 @@ __global__ __launch_bounds__(NTH) void attn_bwd_kernel(const T* __restrict__ dct
     }
   }
   __syncthreads();
-  stage(R2, k, krow0, ldk, hoff, LK, lk, hd);
+  stage_store(R2, nch, LK, hd);
   __syncthreads();
+  stage_load(nch, q, qrow0, ldq, hoff, LQ, lq, hd);  // Q's loads fly during phases 2-3
   // phase 2: dQ = scale * dS K
   {
     const int tq = LQ >> 5, td = hd >> 5;
@@ -224,14 +297,23 @@ __global__ __launch_bounds__(NTH) void attn_bwd_kernel(const T* __restrict__ dct
   }
   __syncthreads();
   // phase 3: R2 <- Pd [LQ][LK]; dV = Pd^T dO
-  for (int e = threadIdx.x; e < LQ * LK; e += NTH) {
-    const int i = e / LK, j = e - (e / LK) * LK;
-    float pd = 0.f;
-    if (i < lq && j < lk) {
-      const long long pidx = pbase + (long long)i * lk + j;
-      pd = probs[pidx] * k3m_dropout_scale(seed, off + pidx, p_drop);
+  {
+    constexpr int U = MAXL * MAXL / NTH;
+    float pv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {   // all loads first
+      const int e = threadIdx.x + u * NTH;
+      const int i = e / LK, j = e - i * LK;
+      pv[u] = (e < LQ * LK && i < lq && j < lk) ? probs[pbase + (long long)i * lk + j] : 0.f;
     }
-    R2[sw(i, j, LK)] = pd;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = threadIdx.x + u * NTH;
+      if (e < LQ * LK) {
+        const int i = e / LK, j = e - i * LK;
+        R2[sw(i, j, LK)] = pv[u] * k3m_dropout_scale(seed, off + pbase + (long long)i * lk + j, p_drop);
+      }
+    }
   }
   __syncthreads();
   {
@@ -255,7 +337,7 @@ __global__ __launch_bounds__(NTH) void attn_bwd_kernel(const T* __restrict__ dct
   }
   __syncthreads();
   // phase 4: R1 <- Q; dK = scale * dS^T Q
-  stage(R1, q, qrow0, ldq, hoff, LQ, lq, hd);
+  stage_store(R1, nch, LQ, hd);
   __syncthreads();
   {
     const int tk = LK >> 5, td = hd >> 5;
@@ -290,6 +372,12 @@ size_t bwd_lds(int lq, int lk, int hd) {
 
 constexpr int LDS_MAX = 160 * 1024;
 
+// the staging loads are 16-byte vectors along each row's head slice
+bool vec_ok(const void* p, long long ld, int dtype) {
+  const int ve = dtype == K3M_BF16 ? 8 : 4;
+  return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % ve == 0;
+}
+
 template <typename T>
 void set_lds_attr() {
   static bool done = false;
@@ -309,6 +397,7 @@ extern "C" int k3m_attn_fwd(const void* q, long long ldq, const void* k, long lo
   K3M_ARG(q && k && v && ctx && probs);
   K3M_ARG(lq > 0 && lq <= MAXL && lk > 0 && lk <= MAXL && hd > 0 && hd <= MAXD && hd % 32 == 0 && nh > 0);
   if (nseq == 0) return 0;
+  K3M_ARG(vec_ok(q, ldq, dtype) && vec_ok(k, ldk, dtype) && vec_ok(v, ldv, dtype));
   const size_t lds = fwd_lds(lq, lk, hd);
   K3M_ARG(lds <= (size_t)LDS_MAX);
   if (dtype == K3M_F32) {
@@ -336,6 +425,7 @@ extern "C" int k3m_attn_bwd(const void* dctx, long long ldc, const void* o, long
   K3M_ARG(dctx && o && q && k && v && probs && dq && dk && dv);
   K3M_ARG(lq > 0 && lq <= MAXL && lk > 0 && lk <= MAXL && hd > 0 && hd <= MAXD && hd % 32 == 0 && nh > 0);
   if (nseq == 0) return 0;
+  K3M_ARG(vec_ok(q, ldq, dtype) && vec_ok(k, ldk, dtype) && vec_ok(v, ldv, dtype) && vec_ok(dctx, ldc, dtype));
   const size_t lds = bwd_lds(lq, lk, hd);
   K3M_ARG(lds <= (size_t)LDS_MAX);
   if (dtype == K3M_F32) {

@@ -1,0 +1,450 @@
+// bf16 fused attention for the short K3M sequences (L <= 128, head dim 64 or 128) on
+// v_mfma_f32_32x32x16_bf16 — the mixed-precision encoder's attention.
+//
+// One workgroup (4 waves) per (sequence, head); Q, K, V (and dO) live in LDS as bf16 row-major
+// images, 16-B chunk c of row r stored at slot c ^ swz(r) so that both kinds of operand read are
+// bank-conflict-free: ds_read_b128 row reads (32 rows x one chunk) and gfx950's transposing
+// ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane group).
+//
+// Forward, wave w owns query tile i in [32w, 32w+32):
+//   S^T = K Q^T  (A = K rows, B = Q rows; the tile has keys j on the registers and the query i
+//                 on the lane, so the softmax over j is in-register + one lane-half exchange)
+//   P   = softmax_j(scale S + mask), dropout, row log-sum-exp saved (no L x L probabilities in HBM)
+//   O   = P V    (the bf16-converted P registers ARE the A operand — k order permuted as the
+//                 accumulator map dictates — and V's B fragments come from transposed reads)
+// Backward, wave w first owns query tile i (phase A), then key tile j (phase B):
+//   A: recompute S^T and P from the saved LSE, dP^T = V dO^T, dS = P (mask dP - D), write
+//      P_drop and dS as bf16 [i][j] images; dQ = scale dS K from registers (as in the forward).
+//   B: dV = P_drop^T dO and dK = scale dS^T Q with both operands read transposed from LDS.
+// Semantics are those of attention.hip (vilbert_k3m.py:449-464 etc.) with the same dropout counter
+// (seed, off + ((s nh + h) lq + i) lk + j), so a mask drawn by one kernel is the other's mask.
+#include "common.h"
+
+namespace {
+
+constexpr int NW = 4, NT = NW * 64;
+constexpr int MAXL = 128;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef short short8v __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) short4v lds_short4v;
+
+// element offset of chunk c (8 bf16) of row r in an image whose rows hold NC chunks
+template <int NC>
+__device__ __forceinline__ int ioff(int r, int c) {
+  if constexpr (NC == 16) return r * 128 + ((c ^ (((r & 3) << 2) | ((r >> 2) & 3))) << 3);
+  else if constexpr (NC == 8) return r * 64 + ((c ^ ((((r >> 1) & 1) << 2) | ((r >> 2) & 3))) << 3);
+  else return r * 32 + (c << 3);  // NC == 4: 64-B rows, the four rows of a transposed read never collide
+}
+
+__device__ __forceinline__ uint16_t bf_bits(float x) { return __builtin_bit_cast(uint16_t, (__bf16)x); }
+
+// row fragment: X[rbase + (lane&31)][16 ks + 8 (lane>>5) .. +7]
+template <int NC>
+__device__ __forceinline__ bf16x8 rowfrag(const uint16_t* img, int rbase, int ks, int lane) {
+  return *reinterpret_cast<const bf16x8*>(img + ioff<NC>(rbase + (lane & 31), 2 * ks + (lane >> 5)));
+}
+
+// transposed fragment: element e of lane l = X[row(e)][cbase + (l&31)] with
+//   PERM = false: row(e) = rbase + 8h + e                     (natural MFMA k order)
+//   PERM = true:  row(e) = rbase + 8(e>>2) + 4h + (e&3)       (accumulator-as-operand k order)
+template <int NC, bool PERM>
+__device__ __forceinline__ bf16x8 trfrag(const uint16_t* img, int rbase, int cbase, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, h = lane >> 5;
+  const int ch = ((cbase + 16 * (g & 1)) >> 3) + (p >> 1);
+  const int r0 = PERM ? rbase + 4 * h + q : rbase + 8 * h + q;
+  const int r1 = PERM ? r0 + 8 : r0 + 4;
+  const short4v x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(img + ioff<NC>(r0, ch) + 4 * (p & 1)));
+  const short4v x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(img + ioff<NC>(r1, ch) + 4 * (p & 1)));
+  const short8v v = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// accumulator registers 8s..8s+7 as a bf16 operand fragment (k order: see trfrag PERM)
+__device__ __forceinline__ bf16x8 accfrag(const floatx16& a, int s) {
+  bf16x8 f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = (__bf16)a[8 * s + e];
+  return f;
+}
+
+__device__ __forceinline__ floatx16 zero16() {
+  floatx16 z;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) z[r] = 0.f;
+  return z;
+}
+
+// stage rows [row0, row0 + nrows) x [coff, coff + 8 NC) of a bf16 matrix into an image
+// (rows >= nvalid zero); all loads issued before the LDS writes
+template <int NC>
+__device__ __forceinline__ void stage(uint16_t* img, const uint16_t* __restrict__ src, long long row0, long long ld,
+                                      int coff, int nrows, int nvalid) {
+  constexpr int U = MAXL * NC / NT;
+  uint4 r[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = threadIdx.x + u * NT;
+    const int i = e / NC, c = e % NC;
+    r[u] = make_uint4(0u, 0u, 0u, 0u);
+    if (i < nvalid) r[u] = *reinterpret_cast<const uint4*>(src + (row0 + i) * ld + coff + 8 * c);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = threadIdx.x + u * NT;
+    const int i = e / NC, c = e % NC;
+    if (i < nrows) *reinterpret_cast<uint4*>(img + ioff<NC>(i, c)) = r[u];
+  }
+}
+
+// ------------------------------------------------------------------ forward
+template <int HD>
+__global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __restrict__ q, long long ldq,
+                                                          const uint16_t* __restrict__ k, long long ldk,
+                                                          const uint16_t* __restrict__ v, long long ldv,
+                                                          const float* __restrict__ kmask, uint16_t* __restrict__ ctx,
+                                                          long long ldc, float* __restrict__ lse, int lq, int lk,
+                                                          int nh, float scale, float p_drop, uint64_t seed,
+                                                          uint64_t off) {
+  constexpr int NC = HD / 8, DT = HD / 32, KS = HD / 16;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int s = blockIdx.x / nh, h = blockIdx.x % nh;
+  const int LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
+  uint16_t* Qs = smem;
+  uint16_t* Ks = Qs + LQ * HD;
+  uint16_t* Vs = Ks + LK * HD;
+  float* msk = reinterpret_cast<float*>(Vs + LK * HD);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
+  const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
+  const int hoff = h * HD;
+
+  stage<NC>(Qs, q, qrow0, ldq, hoff, LQ, lq);
+  stage<NC>(Ks, k, krow0, ldk, hoff, LK, lk);
+  stage<NC>(Vs, v, krow0, ldv, hoff, LK, lk);
+  for (int j = threadIdx.x; j < LK; j += NT) msk[j] = j < lk ? (kmask ? kmask[krow0 + j] : 0.f) : -INFINITY;
+  __syncthreads();
+  const int i0 = 32 * w;
+  if (i0 >= LQ) return;
+  const int NJT = LK / 32;
+  floatx16 S[MAXL / 32];
+#pragma unroll
+  for (int jt = 0; jt < MAXL / 32; ++jt) {
+    if (jt < NJT) {
+      floatx16 a = zero16();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag<NC>(Ks, 32 * jt, ks, lane), rowfrag<NC>(Qs, i0, ks, lane),
+                                                     a, 0, 0, 0);
+      S[jt] = a;
+    }
+  }
+  // softmax over j (registers x lane halves) for query i = i0 + cl
+  const int i = i0 + cl;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int jt = 0; jt < MAXL / 32; ++jt)
+    if (jt < NJT) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = 32 * jt + (r & 3) + 8 * (r >> 2) + 4 * kl;
+        const float x = S[jt][r] * scale + msk[j];
+        S[jt][r] = x;
+        mx = fmaxf(mx, x);
+      }
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int jt = 0; jt < MAXL / 32; ++jt)
+    if (jt < NJT) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = __expf(S[jt][r] - mx);
+        S[jt][r] = e;
+        sum += e;
+      }
+    }
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.f / sum;
+  const long long prow = ((long long)s * nh + h) * lq + i;   // row of the [nseq, nh, lq] LSE
+  if (kl == 0 && i < lq) lse[prow] = mx + __logf(sum);
+  const long long pbase = prow * lk;
+#pragma unroll
+  for (int jt = 0; jt < MAXL / 32; ++jt)
+    if (jt < NJT) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = 32 * jt + (r & 3) + 8 * (r >> 2) + 4 * kl;
+        float pv = S[jt][r] * inv;
+        if (p_drop > 0.f) pv *= (i < lq && j < lk) ? k3m_dropout_scale(seed, off + pbase + j, p_drop) : 0.f;
+        S[jt][r] = pv;
+      }
+    }
+  // O = P V
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    floatx16 o = zero16();
+#pragma unroll
+    for (int jt = 0; jt < MAXL / 32; ++jt)
+      if (jt < NJT) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(accfrag(S[jt], s2), trfrag<NC, true>(Vs, 32 * jt + 16 * s2, 32 * dt, lane),
+                                                       o, 0, 0, 0);
+      }
+    // o[r] = O[i0 + (r&3) + 8(r>>2) + 4kl][32 dt + cl]
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ii = i0 + (r & 3) + 8 * (r >> 2) + 4 * kl;
+      if (ii < lq) ctx[(qrow0 + ii) * ldc + hoff + 32 * dt + cl] = bf_bits(o[r]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ backward
+template <int HD>
+__global__ __launch_bounds__(NT, 1) void flash_bwd_kernel(const uint16_t* __restrict__ dctx, long long ldc,
+                                                          const uint16_t* __restrict__ o, long long ldo,
+                                                          const uint16_t* __restrict__ q, long long ldq,
+                                                          const uint16_t* __restrict__ k, long long ldk,
+                                                          const uint16_t* __restrict__ v, long long ldv,
+                                                          const float* __restrict__ kmask, const float* __restrict__ lse,
+                                                          uint16_t* __restrict__ dq, uint16_t* __restrict__ dk,
+                                                          uint16_t* __restrict__ dv, long long lddq, long long lddk,
+                                                          long long lddv, int lq, int lk, int nh, float scale,
+                                                          float p_drop, uint64_t seed, uint64_t off) {
+  constexpr int NC = HD / 8, DT = HD / 32, KS = HD / 16;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int s = blockIdx.x / nh, h = blockIdx.x % nh;
+  const int LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
+  const int PW = LK == 96 ? 128 : LK;          // row width of the P / dS images (NC 4, 8 or 16)
+  uint16_t* Qs = smem;
+  uint16_t* dOs = Qs + LQ * HD;
+  uint16_t* Ks = dOs + LQ * HD;
+  uint16_t* Vs = Ks + LK * HD;
+  uint16_t* Ps = Vs + LK * HD;                 // [LQ][PW] P_drop
+  uint16_t* dSs = Ps + LQ * PW;                // [LQ][PW] dS
+  float* msk = reinterpret_cast<float*>(dSs + LQ * PW);
+  float* Ls = msk + LK;
+  float* Ds = Ls + LQ;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
+  const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
+  const int hoff = h * HD;
+  const long long lrow0 = ((long long)s * nh + h) * lq;
+
+  stage<NC>(Qs, q, qrow0, ldq, hoff, LQ, lq);
+  stage<NC>(dOs, dctx, qrow0, ldc, hoff, LQ, lq);
+  stage<NC>(Ks, k, krow0, ldk, hoff, LK, lk);
+  stage<NC>(Vs, v, krow0, ldv, hoff, LK, lk);
+  for (int j = threadIdx.x; j < LK; j += NT) msk[j] = j < lk ? (kmask ? kmask[krow0 + j] : 0.f) : -INFINITY;
+  {
+    // D_i = dO_i . O_i: two threads per row, each over half of the head dimension (16-B loads)
+    const int ii = threadIdx.x >> 1, half = threadIdx.x & 1;
+    float acc = 0.f;
+    if (ii < lq) {
+      const uint16_t* pd = dctx + (qrow0 + ii) * ldc + hoff + half * (HD / 2);
+      const uint16_t* po = o + (qrow0 + ii) * ldo + hoff + half * (HD / 2);
+      uint4 a[HD / 16], b[HD / 16];
+#pragma unroll
+      for (int c = 0; c < HD / 16; ++c) {
+        a[c] = *reinterpret_cast<const uint4*>(pd + 8 * c);
+        b[c] = *reinterpret_cast<const uint4*>(po + 8 * c);
+      }
+#pragma unroll
+      for (int c = 0; c < HD / 16; ++c) {
+        const uint32_t wa[4] = {a[c].x, a[c].y, a[c].z, a[c].w}, wb[4] = {b[c].x, b[c].y, b[c].z, b[c].w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          acc += __uint_as_float(wa[t] << 16) * __uint_as_float(wb[t] << 16) +
+                 __uint_as_float(wa[t] & 0xffff0000u) * __uint_as_float(wb[t] & 0xffff0000u);
+      }
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    if (half == 0 && ii < LQ) {
+      Ds[ii] = acc;
+      Ls[ii] = ii < lq ? lse[lrow0 + ii] : 0.f;
+    }
+  }
+  __syncthreads();
+
+  const int NJT = LK / 32;
+  // ---- phase A: wave w owns query tile i0 = 32 w
+  const int i0 = 32 * w;
+  if (i0 < LQ) {
+    const int i = i0 + cl;
+    const float li = Ls[i], di = Ds[i];
+    const bool iv = i < lq;
+    const long long pbase = (lrow0 + i) * lk;
+    floatx16 dQ[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) dQ[dt] = zero16();
+#pragma unroll
+    for (int jt = 0; jt < MAXL / 32; ++jt) {
+      if (jt >= NJT) break;
+      floatx16 St = zero16(), dP = zero16();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        St = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag<NC>(Ks, 32 * jt, ks, lane), rowfrag<NC>(Qs, i0, ks, lane),
+                                                      St, 0, 0, 0);
+        dP = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag<NC>(Vs, 32 * jt, ks, lane), rowfrag<NC>(dOs, i0, ks, lane),
+                                                      dP, 0, 0, 0);
+      }
+      floatx16 pd, ds;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = 32 * jt + (r & 3) + 8 * (r >> 2) + 4 * kl;
+        const float p = iv ? __expf(St[r] * scale + msk[j] - li) : 0.f;
+        const float dm = (p_drop > 0.f && iv && j < lk) ? k3m_dropout_scale(seed, off + pbase + j, p_drop) : 1.f;
+        pd[r] = p * dm;
+        ds[r] = p * (dP[r] * dm - di);
+      }
+      // P_drop and dS -> [i][j] images: registers 4g..4g+3 are 4 consecutive keys (8 bytes)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = 4 * jt + g;   // chunk of keys 32 jt + 8 g .. +7; this lane half holds 4 kl .. 4 kl + 3
+        uint2 wp, wd;
+        wp.x = bf_bits(pd[4 * g]) | ((uint32_t)bf_bits(pd[4 * g + 1]) << 16);
+        wp.y = bf_bits(pd[4 * g + 2]) | ((uint32_t)bf_bits(pd[4 * g + 3]) << 16);
+        wd.x = bf_bits(ds[4 * g]) | ((uint32_t)bf_bits(ds[4 * g + 1]) << 16);
+        wd.y = bf_bits(ds[4 * g + 2]) | ((uint32_t)bf_bits(ds[4 * g + 3]) << 16);
+        int po;
+        if (PW == 128) po = ioff<16>(i, c);
+        else if (PW == 64) po = ioff<8>(i, c);
+        else po = ioff<4>(i, c);
+        *reinterpret_cast<uint2*>(Ps + po + 4 * kl) = wp;
+        *reinterpret_cast<uint2*>(dSs + po + 4 * kl) = wd;
+      }
+      // dQ += dS K (dS registers as the A operand, K transposed)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 a = accfrag(ds, s2);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+          dQ[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, trfrag<NC, true>(Ks, 32 * jt + 16 * s2, 32 * dt, lane),
+                                                            dQ[dt], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ii = i0 + (r & 3) + 8 * (r >> 2) + 4 * kl;
+        if (ii < lq) dq[(qrow0 + ii) * lddq + hoff + 32 * dt + cl] = bf_bits(dQ[dt][r] * scale);
+      }
+  }
+  __syncthreads();
+  // ---- phase B: wave w owns key tile j0 = 32 w: dV = P_drop^T dO, dK = scale dS^T Q
+  const int j0 = 32 * w;
+  if (j0 >= LK) return;
+  floatx16 dV[DT], dK[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    dV[dt] = zero16();
+    dK[dt] = zero16();
+  }
+  for (int ik = 0; ik < LQ / 16; ++ik) {
+    bf16x8 ap, as;
+    if (PW == 128) {
+      ap = trfrag<16, false>(Ps, 16 * ik, j0, lane);
+      as = trfrag<16, false>(dSs, 16 * ik, j0, lane);
+    } else if (PW == 64) {
+      ap = trfrag<8, false>(Ps, 16 * ik, j0, lane);
+      as = trfrag<8, false>(dSs, 16 * ik, j0, lane);
+    } else {
+      ap = trfrag<4, false>(Ps, 16 * ik, j0, lane);
+      as = trfrag<4, false>(dSs, 16 * ik, j0, lane);
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      dV[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap, trfrag<NC, false>(dOs, 16 * ik, 32 * dt, lane), dV[dt], 0, 0, 0);
+      dK[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as, trfrag<NC, false>(Qs, 16 * ik, 32 * dt, lane), dK[dt], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int j = j0 + (r & 3) + 8 * (r >> 2) + 4 * kl;
+      if (j < lk) {
+        dv[(krow0 + j) * lddv + hoff + 32 * dt + cl] = bf_bits(dV[dt][r]);
+        dk[(krow0 + j) * lddk + hoff + 32 * dt + cl] = bf_bits(dK[dt][r] * scale);
+      }
+    }
+}
+
+size_t fwd_lds(int lq, int lk, int hd) {
+  const size_t LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
+  return 2 * (LQ * hd + 2 * LK * hd) + 4 * LK;
+}
+size_t bwd_lds(int lq, int lk, int hd) {
+  const size_t LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
+  const size_t PW = LK == 96 ? 128 : LK;
+  return 2 * (2 * LQ * hd + 2 * LK * hd + 2 * LQ * PW) + 4 * (LK + 2 * LQ);
+}
+
+constexpr int LDS_MAX = 160 * 1024;
+
+void set_attrs() {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)flash_fwd_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_fwd_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_bwd_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_bwd_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    done = true;
+  }
+}
+
+bool vec_ok(const void* p, long long ld) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 8 == 0; }
+
+}  // namespace
+
+extern "C" int k3m_flash_attn_fwd(const void* q, long long ldq, const void* k, long long ldk, const void* v,
+                                  long long ldv, const float* kmask, void* ctx, long long ldc, float* lse, int nseq,
+                                  int lq, int lk, int nh, int hd, float scale, float p_drop, uint64_t seed,
+                                  uint64_t off, hipStream_t st) {
+  K3M_ARG(q && k && v && ctx && lse);
+  K3M_ARG(lq > 0 && lq <= MAXL && lk > 0 && lk <= MAXL && (hd == 64 || hd == 128) && nh > 0 && nseq >= 0);
+  K3M_ARG(vec_ok(q, ldq) && vec_ok(k, ldk) && vec_ok(v, ldv));
+  if (nseq == 0) return 0;
+  const size_t lds = fwd_lds(lq, lk, hd);
+  K3M_ARG(lds <= (size_t)LDS_MAX);
+  set_attrs();
+  if (hd == 64)
+    hipLaunchKernelGGL(flash_fwd_kernel<64>, dim3(nseq * nh), dim3(NT), lds, st, (const uint16_t*)q, ldq,
+                       (const uint16_t*)k, ldk, (const uint16_t*)v, ldv, kmask, (uint16_t*)ctx, ldc, lse, lq, lk, nh,
+                       scale, p_drop, seed, off);
+  else
+    hipLaunchKernelGGL(flash_fwd_kernel<128>, dim3(nseq * nh), dim3(NT), lds, st, (const uint16_t*)q, ldq,
+                       (const uint16_t*)k, ldk, (const uint16_t*)v, ldv, kmask, (uint16_t*)ctx, ldc, lse, lq, lk, nh,
+                       scale, p_drop, seed, off);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_flash_attn_bwd(const void* dctx, long long ldc, const void* o, long long ldo, const void* q,
+                                  long long ldq, const void* k, long long ldk, const void* v, long long ldv,
+                                  const float* kmask, const float* lse, void* dq, void* dk, void* dv, long long lddq,
+                                  long long lddk, long long lddv, int nseq, int lq, int lk, int nh, int hd,
+                                  float scale, float p_drop, uint64_t seed, uint64_t off, hipStream_t st) {
+  K3M_ARG(dctx && o && q && k && v && lse && dq && dk && dv);
+  K3M_ARG(lq > 0 && lq <= MAXL && lk > 0 && lk <= MAXL && (hd == 64 || hd == 128) && nh > 0 && nseq >= 0);
+  K3M_ARG(vec_ok(q, ldq) && vec_ok(k, ldk) && vec_ok(v, ldv) && vec_ok(dctx, ldc) && vec_ok(o, ldo));
+  if (nseq == 0) return 0;
+  const size_t lds = bwd_lds(lq, lk, hd);
+  K3M_ARG(lds <= (size_t)LDS_MAX);
+  set_attrs();
+  if (hd == 64)
+    hipLaunchKernelGGL(flash_bwd_kernel<64>, dim3(nseq * nh), dim3(NT), lds, st, (const uint16_t*)dctx, ldc,
+                       (const uint16_t*)o, ldo, (const uint16_t*)q, ldq, (const uint16_t*)k, ldk, (const uint16_t*)v,
+                       ldv, kmask, lse, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, lddq, lddk, lddv, lq, lk, nh,
+                       scale, p_drop, seed, off);
+  else
+    hipLaunchKernelGGL(flash_bwd_kernel<128>, dim3(nseq * nh), dim3(NT), lds, st, (const uint16_t*)dctx, ldc,
+                       (const uint16_t*)o, ldo, (const uint16_t*)q, ldq, (const uint16_t*)k, ldk, (const uint16_t*)v,
+                       ldv, kmask, lse, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, lddq, lddk, lddv, lq, lk, nh,
+                       scale, p_drop, seed, off);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}

@@ -24,6 +24,7 @@ constexpr int BK = 64, NT = 256;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef short short8v __attribute__((ext_vector_type(8)));
 
 // element offset (bf16 units) of k-chunk c (8 bf16) of row r in a swizzled [TILE][64] image
 __device__ __forceinline__ int swz(int r, int c) { return r * BK + ((c ^ ((r >> 1) & 7)) << 3); }
@@ -31,18 +32,31 @@ __device__ __forceinline__ int swz(int r, int c) { return r * BK + ((c ^ ((r >> 
 __device__ __forceinline__ uint32_t lo_pair(uint32_t a, uint32_t b) { return (a & 0xffffu) | (b << 16); }
 __device__ __forceinline__ uint32_t hi_pair(uint32_t a, uint32_t b) { return (a >> 16) | (b & 0xffff0000u); }
 
-template <bool KC, int TILE>
+// Operand staging modes.
+//   KC  (0): K-contiguous operand -> swizzled [TILE][64] image, fragments by ds_read_b128.
+//   MNR (1): MN-contiguous, TILE = 64 -> transposed in registers into the same [TILE][64] image.
+//   MNT (2): MN-contiguous, TILE = 128 -> copied as-is into a [64 k][128 mn] image of 256-B rows
+//            (16-B chunk ch of row k at slot ch ^ (((k&3)<<2) | ((k>>2)&3))) and read with the
+//            gfx950 transposing ds_read_b64_tr_b16 (two per fragment): no register transpose and
+//            4 ds_write_b128 per thread instead of 8 ds_write_b64.
+enum { KC = 0, MNR = 1, MNT = 2 };
+
+template <int MODE, int TILE>
 struct Stage {
-  static constexpr int NR = KC ? TILE / 32 : 4;
+  static constexpr int NR = MODE == MNR ? 4 : TILE / 32;
   u32x4 r[NR];
 };
 
+__device__ __forceinline__ int mnt_off(int k, int ch) {  // element offset in the MNT image
+  return k * 128 + ((ch ^ (((k & 3) << 2) | ((k >> 2) & 3))) << 3);
+}
+
 // Load the (TILE x BK) tile at (mn0, k0) into registers.
-template <bool KC, bool VEC, int TILE>
+template <int MODE, bool VEC, int TILE>
 __device__ __forceinline__ void load_tile(const uint16_t* __restrict__ p, long long ld, int mn0, int k0, int MN,
-                                          int K, Stage<KC, TILE>& s) {
+                                          int K, Stage<MODE, TILE>& s) {
   const int t = threadIdx.x;
-  if constexpr (KC) {
+  if constexpr (MODE == KC) {
 #pragma unroll
     for (int it = 0; it < TILE / 32; ++it) {
       const int idx = t + NT * it;
@@ -57,6 +71,27 @@ __device__ __forceinline__ void load_tile(const uint16_t* __restrict__ p, long l
         for (int q = 0; q < 4; ++q) {
           const uint32_t e0 = (gm < MN && gk + 2 * q < K) ? p[(long long)gm * ld + gk + 2 * q] : 0u;
           const uint32_t e1 = (gm < MN && gk + 2 * q + 1 < K) ? p[(long long)gm * ld + gk + 2 * q + 1] : 0u;
+          w[q] = e0 | (e1 << 16);
+        }
+        s.r[it] = u32x4{w[0], w[1], w[2], w[3]};
+      }
+    }
+  } else if constexpr (MODE == MNT) {
+    static_assert(TILE == 128, "MNT images are 128 wide");
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int idx = t + NT * it;
+      const int kr = idx >> 4, ch = idx & 15;
+      const int gk = k0 + kr, gm = mn0 + ch * 8;
+      if constexpr (VEC) {
+        s.r[it] = (gk < K && gm < MN) ? *reinterpret_cast<const u32x4*>(p + (long long)gk * ld + gm)
+                                      : u32x4{0u, 0u, 0u, 0u};
+      } else {
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t e0 = (gk < K && gm + 2 * q < MN) ? p[(long long)gk * ld + gm + 2 * q] : 0u;
+          const uint32_t e1 = (gk < K && gm + 2 * q + 1 < MN) ? p[(long long)gk * ld + gm + 2 * q + 1] : 0u;
           w[q] = e0 | (e1 << 16);
         }
         s.r[it] = u32x4{w[0], w[1], w[2], w[3]};
@@ -87,14 +122,20 @@ __device__ __forceinline__ void load_tile(const uint16_t* __restrict__ p, long l
   }
 }
 
-template <bool KC, int TILE>
-__device__ __forceinline__ void store_tile(uint16_t* __restrict__ lds, const Stage<KC, TILE>& s) {
+template <int MODE, int TILE>
+__device__ __forceinline__ void store_tile(uint16_t* __restrict__ lds, const Stage<MODE, TILE>& s) {
   const int t = threadIdx.x;
-  if constexpr (KC) {
+  if constexpr (MODE == KC) {
 #pragma unroll
     for (int it = 0; it < TILE / 32; ++it) {
       const int idx = t + NT * it;
       *reinterpret_cast<u32x4*>(lds + swz(idx >> 3, idx & 7)) = s.r[it];
+    }
+  } else if constexpr (MODE == MNT) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int idx = t + NT * it;
+      *reinterpret_cast<u32x4*>(lds + mnt_off(idx >> 4, idx & 15)) = s.r[it];
     }
   } else {
     constexpr int G8 = TILE / 8;
@@ -109,6 +150,30 @@ __device__ __forceinline__ void store_tile(uint16_t* __restrict__ lds, const Sta
       *reinterpret_cast<u32x2*>(lds + swz(mn, c) + half) = e;
       *reinterpret_cast<u32x2*>(lds + swz(mn + 1, c) + half) = o;
     }
+  }
+}
+
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) short4v lds_short4v;
+
+// MFMA operand fragment of the 32-wide sub-tile at mn_base, k-step ks: lane l gets
+// X[mn_base + (l&31)][16 ks + 8 (l>>5) + j], j = 0..7.
+template <int MODE>
+__device__ __forceinline__ bf16x8 frag(const uint16_t* img, int mn_base, int ks, int lane) {
+  if constexpr (MODE == MNT) {
+    // two 4(k) x 16(mn) transposed block reads per 16-lane group g: rows 16ks + 8h + 4t + q,
+    // columns cb .. cb+15; lane 4q+p addresses row q, columns cb + 4p .. +3 (T10 in the guide)
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, h = lane >> 5;
+    const int ch = ((mn_base + 16 * (g & 1)) >> 3) + (p >> 1);
+    const int r0 = 16 * ks + 8 * h + q;
+    const short4v x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_short4v*)(img + mnt_off(r0, ch) + 4 * (p & 1)));
+    const short4v x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_short4v*)(img + mnt_off(r0 + 4, ch) + 4 * (p & 1)));
+    const short8v v = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  } else {
+    return *reinterpret_cast<const bf16x8*>(img + swz(mn_base + (lane & 31), 2 * ks + (lane >> 5)));
   }
 }
 
@@ -179,14 +244,16 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(K3mGemm g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  Stage<AK, TBM> ra;
-  Stage<BK_, TBN> rb;
+  constexpr int AM = AK ? KC : (TBM == 128 ? MNT : MNR);
+  constexpr int BM_ = BK_ ? KC : (TBN == 128 ? MNT : MNR);
+  Stage<AM, TBM> ra;
+  Stage<BM_, TBN> rb;
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   if (nk > 0) {
-    load_tile<AK, VEC, TBM>(A, g.lda, m0, kbeg, M, kend, ra);
-    load_tile<BK_, VEC, TBN>(B, g.ldb, n0, kbeg, N, kend, rb);
-    store_tile<AK, TBM>(smem, ra);
-    store_tile<BK_, TBN>(smem + TBM * BK, rb);
+    load_tile<AM, VEC, TBM>(A, g.lda, m0, kbeg, M, kend, ra);
+    load_tile<BM_, VEC, TBN>(B, g.ldb, n0, kbeg, N, kend, rb);
+    store_tile<AM, TBM>(smem, ra);
+    store_tile<BM_, TBN>(smem + TBM * BK, rb);
   }
   __syncthreads();
   const int kl = lane >> 5, cl = lane & 31;
@@ -195,8 +262,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(K3mGemm g) {
     const bool more = kt + 1 < nk;
     if (more) {
       const int k0 = kbeg + (kt + 1) * BK;
-      load_tile<AK, VEC, TBM>(A, g.lda, m0, k0, M, kend, ra);
-      load_tile<BK_, VEC, TBN>(B, g.ldb, n0, k0, N, kend, rb);
+      load_tile<AM, VEC, TBM>(A, g.lda, m0, k0, M, kend, ra);
+      load_tile<BM_, VEC, TBN>(B, g.ldb, n0, k0, N, kend, rb);
     }
     const uint16_t* as = smem + cur * BUF;
     const uint16_t* bs = as + TBM * BK;
@@ -204,17 +271,17 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(K3mGemm g) {
     for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8 a[FM], b[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const bf16x8*>(as + swz(wm + 32 * i + cl, 2 * ks + kl));
+      for (int i = 0; i < FM; ++i) a[i] = frag<AM>(as, wm + 32 * i, ks, lane);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const bf16x8*>(bs + swz(wn + 32 * j + cl, 2 * ks + kl));
+      for (int j = 0; j < FN; ++j) b[j] = frag<BM_>(bs, wn + 32 * j, ks, lane);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     if (more) {
-      store_tile<AK, TBM>(smem + (cur ^ 1) * BUF, ra);
-      store_tile<BK_, TBN>(smem + (cur ^ 1) * BUF + TBM * BK, rb);
+      store_tile<AM, TBM>(smem + (cur ^ 1) * BUF, ra);
+      store_tile<BM_, TBN>(smem + (cur ^ 1) * BUF + TBM * BK, rb);
     }
     __syncthreads();
   }

@@ -33,6 +33,16 @@ __device__ __forceinline__ void st4<bf16_t>(bf16_t* p, floatx4 v) {
   *reinterpret_cast<uint2*>(p) = u;
 }
 
+// value as stored in T (identity for fp32, round-to-nearest bf16 otherwise)
+template <typename T>
+__device__ __forceinline__ floatx4 round4(floatx4 v) {
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = to_f(from_f<bf16_t>(v[q]));
+  }
+  return v;
+}
+
 // ------------------------------------------------------------------ LayerNorm forward
 template <typename T>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ res,
@@ -90,22 +100,25 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 }
 
 // ------------------------------------------------------------------ LayerNorm backward
-constexpr int LN_BWD_BLOCKS = 128;
+constexpr int LN_BWD_BLOCKS = K3M_LN_BWD_SLABS;
 
 template <typename T>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ xhat,
                                                      const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                      T* __restrict__ dres, T* __restrict__ dx, float* __restrict__ ws,
                                                      int rows, int cols, float p_in, float p_out, uint64_t seed,
-                                                     uint64_t off_in, uint64_t off_out, int acc_res) {
-  __shared__ float red[2][4][1024];
+                                                     uint64_t off_in, uint64_t off_out, int acc_res, int want_sum) {
+  // column partials of dgamma, dbeta and (want_sum) sum(dx): per wave in registers, then one
+  // [3][cols] slab per block through LDS (reduced by slab_sum_kernel)
+  __shared__ float red[4][1024];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nv = cols >> 8;
-  floatx4 pg[MAXV], pb[MAXV];
+  floatx4 pg[MAXV], pb[MAXV], px[MAXV];
 #pragma unroll
   for (int j = 0; j < MAXV; ++j) {
     pg[j] = floatx4{0.f, 0.f, 0.f, 0.f};
     pb[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    px[j] = floatx4{0.f, 0.f, 0.f, 0.f};
   }
   for (int row = blockIdx.x * 4 + w; row < rows; row += gridDim.x * 4) {
     const long long base = (long long)row * cols;
@@ -148,23 +161,24 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
           }
           st4<T>(dx + base + c, ds);
         }
+        if (want_sum) {   // the sum of dx as stored (bf16-rounded when T is bf16)
+          px[j] += round4<T>(ds);
+        }
       }
   }
-  // combine the 4 waves' column partials, write this block's slab
+  // combine the 4 waves' column partials, write this block's slabs
+  for (int k = 0; k < (want_sum ? 3 : 2); ++k) {
 #pragma unroll
-  for (int j = 0; j < MAXV; ++j)
-    if (j < nv) {
-      const int c = (lane + 64 * j) * 4;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        red[0][w][c + q] = pg[j][q];
-        red[1][w][c + q] = pb[j][q];
+    for (int j = 0; j < MAXV; ++j)
+      if (j < nv) {
+        const int c = (lane + 64 * j) * 4;
+        const floatx4 v = k == 0 ? pg[j] : (k == 1 ? pb[j] : px[j]);
+        *reinterpret_cast<floatx4*>(&red[w][c]) = v;
       }
-    }
-  __syncthreads();
-  for (int c = threadIdx.x; c < cols; c += 256) {
-    ws[(long long)blockIdx.x * cols + c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
-    ws[(long long)(gridDim.x + blockIdx.x) * cols + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+    __syncthreads();
+    for (int c = threadIdx.x; c < cols; c += 256)
+      ws[((long long)k * gridDim.x + blockIdx.x) * cols + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    __syncthreads();
   }
 }
 
@@ -339,7 +353,8 @@ extern "C" int k3m_ln_fwd(const void* x, const void* res, const float* gamma, co
 }
 
 extern "C" int k3m_ln_bwd(const void* dy, const void* xhat, const float* rstd, const float* gamma, void* dres, void* dx,
-                          float* dgamma, float* dbeta, int rows, int cols, float p_in, float p_out, uint64_t seed,
+                          float* dgamma, float* dbeta, float* dxsum, int rows, int cols, float p_in, float p_out,
+                          uint64_t seed,
                           uint64_t off_in, uint64_t off_out, int acc_res, float* ws, int dtype, hipStream_t st) {
   K3M_ARG(dy && xhat && rstd && gamma && dres && dx && dgamma && dbeta && ws);
   K3M_ARG(cols % 256 == 0 && cols <= 1024 && rows >= 0);
@@ -347,11 +362,14 @@ extern "C" int k3m_ln_bwd(const void* dy, const void* xhat, const float* rstd, c
   const int nb = std::min(LN_BWD_BLOCKS, k3m_cdiv(rows, 4));
   DISPATCH_T(dtype, hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3(nb), dim3(256), 0, st, (const T*)dy, (const T*)xhat, rstd,
                                        gamma, (T*)dres, (T*)dx, ws, rows, cols, p_in, p_out, seed, off_in, off_out,
-                                       acc_res));
+                                       acc_res, dxsum != nullptr));
   K3M_CHECK_LAUNCH();
   hipLaunchKernelGGL(slab_sum_kernel, dim3(k3m_cdiv(cols, 32)), dim3(256), 0, st, ws, nb, cols, dgamma, 1);
   hipLaunchKernelGGL(slab_sum_kernel, dim3(k3m_cdiv(cols, 32)), dim3(256), 0, st, ws + (long long)nb * cols, nb, cols,
                      dbeta, 1);
+  if (dxsum)
+    hipLaunchKernelGGL(slab_sum_kernel, dim3(k3m_cdiv(cols, 32)), dim3(256), 0, st, ws + 2LL * nb * cols, nb, cols,
+                       dxsum, 1);
   K3M_CHECK_LAUNCH();
   return 0;
 }

@@ -120,8 +120,9 @@ class Lin(object):
     def fwd(self, x, out=None, epi=None, aux=None, alpha=1.0, beta=0.0):
         return ops.linear(x, self._w(x), self.b, out=out, epi=epi, aux=aux, alpha=alpha, beta=beta)
 
-    def wgrad(self, dy, x, alpha=1.0):
-        ops.linear_wgrad(dy, x, self.gW, self.gb, alpha=alpha)
+    def wgrad(self, dy, x, alpha=1.0, bias_done=False):
+        """bias_done: the bias gradient was already accumulated by dy's producer (k3m_ln_bwd dxsum)."""
+        ops.linear_wgrad(dy, x, self.gW, None if bias_done else self.gb, alpha=alpha)
 
     def dgrad(self, dy, dx=None, beta=0.0, dgelu_aux=None, alpha=1.0):
         return ops.linear_dgrad(dy, self._w(dy), dx=dx, beta=beta, dgelu_aux=dgelu_aux, alpha=alpha)
@@ -150,11 +151,13 @@ class AddLN(object):
         ops.ln_fwd(x, res, self.ln.g, self.ln.b, y, xhat, rstd, p_in=self.p, seed=rng.seed, off_in=off)
         return y, (xhat, rstd, rng.seed, off)
 
-    def bwd(self, dy, saved, dres):
-        """writes d(res) into dres; returns d(x) (aliases dres when dropout is off)."""
+    def bwd(self, dy, saved, dres, dxsum=None):
+        """writes d(res) into dres; returns d(x) (aliases dres when dropout is off).  dxsum: fp32
+        [H] accumulating colsum(d(x)) — the bias gradient of the Linear that produced x."""
         xhat, rstd, seed, off = saved
         dx = dres if self.p == 0 else torch.empty_like(dres)
-        ops.ln_bwd(dy, xhat, rstd, self.ln.g, dres, dx, self.ln.gg, self.ln.gb, p_in=self.p, seed=seed, off_in=off)
+        ops.ln_bwd(dy, xhat, rstd, self.ln.g, dres, dx, self.ln.gg, self.ln.gb, p_in=self.p, seed=seed, off_in=off,
+                   dxsum=dxsum)
         return dx
 
 
@@ -178,26 +181,39 @@ class FFN(object):
     def bwd(self, dy, saved, dh_out=None):
         h, u, f, tsv = saved
         dh = dh_out if dh_out is not None else torch.empty_like(h)
-        do = self.tail.bwd(dy, tsv, dh)
-        self.o.wgrad(do, f)
+        do = self.tail.bwd(dy, tsv, dh, dxsum=self.o.gb)
+        self.o.wgrad(do, f, bias_done=True)
         du = self.o.dgrad(do, dgelu_aux=u)
         self.i.wgrad(du, h)
         self.i.dgrad(du, dx=dh, beta=1.0)
         return dh
 
 
+def _flash(q, hd):
+    # bf16 encoder: the LSE-saving bf16 kernels (attention_bf16.hip); fp32: exact-fp32 kernels
+    return q.dtype == torch.bfloat16 and hd in (64, 128)
+
+
 def _attn_fwd(q, k, v, mask, nseq, lq, lk, nh, p, rng, out=None):
     hd = q.shape[1] // nh
     ctx = out if out is not None else torch.empty((nseq * lq, q.shape[1]), dtype=q.dtype, device=q.device)
-    probs = torch.empty((nseq * nh * lq * lk,), dtype=torch.float32, device=q.device)
-    off = rng.take(probs.numel()) if p > 0 else 0
-    ops.attn_fwd(q, k, v, mask, ctx, probs, nseq, lq, lk, nh, hd, 1.0 / math.sqrt(hd), p, rng.seed, off)
-    return ctx, (probs, nseq, lq, lk, nh, hd, p, rng.seed, off)
+    off = rng.take(nseq * nh * lq * lk) if p > 0 else 0
+    if _flash(q, hd):
+        stat = torch.empty((nseq * nh * lq,), dtype=torch.float32, device=q.device)   # row LSE
+        ops.flash_attn_fwd(q, k, v, mask, ctx, stat, nseq, lq, lk, nh, hd, 1.0 / math.sqrt(hd), p, rng.seed, off)
+    else:
+        stat = torch.empty((nseq * nh * lq * lk,), dtype=torch.float32, device=q.device)   # probabilities
+        ops.attn_fwd(q, k, v, mask, ctx, stat, nseq, lq, lk, nh, hd, 1.0 / math.sqrt(hd), p, rng.seed, off)
+    return ctx, (stat, mask, nseq, lq, lk, nh, hd, p, rng.seed, off)
 
 
 def _attn_bwd(dctx, o, q, k, v, saved, dq, dk, dv):
-    probs, nseq, lq, lk, nh, hd, p, seed, off = saved
-    ops.attn_bwd(dctx, o, q, k, v, probs, dq, dk, dv, nseq, lq, lk, nh, hd, 1.0 / math.sqrt(hd), p, seed, off)
+    stat, mask, nseq, lq, lk, nh, hd, p, seed, off = saved
+    if _flash(q, hd):
+        ops.flash_attn_bwd(dctx, o, q, k, v, mask, stat, dq, dk, dv, nseq, lq, lk, nh, hd, 1.0 / math.sqrt(hd), p,
+                           seed, off)
+    else:
+        ops.attn_bwd(dctx, o, q, k, v, stat, dq, dk, dv, nseq, lq, lk, nh, hd, 1.0 / math.sqrt(hd), p, seed, off)
 
 
 class BertLayerOp(object):
@@ -232,8 +248,8 @@ class BertLayerOp(object):
         M, H = x.shape
         dh1 = self.ffn.bwd(dy, fsv)
         dx = torch.empty_like(x)
-        da = self.tail.bwd(dh1, tsv, dx)
-        self.o.wgrad(da, ctx)
+        da = self.tail.bwd(dh1, tsv, dx, dxsum=self.o.gb)
+        self.o.wgrad(da, ctx, bias_done=True)
         dctx = self.o.dgrad(da)
         dqkv = torch.empty_like(qkv)
         for (r0, nseq, ln, mask), s in zip(segs, asv):
@@ -278,11 +294,11 @@ class ConnectionOp(object):
         s1, s2, q1, q2, ctx1, ctx2, a1s, a2s, t1s, t2s, f1s, f2s, Hb = saved
         dh1 = self.f1.bwd(dy1, f1s)
         dh2 = self.f2.bwd(dy2, f2s)
-        da1 = self.t1.bwd(dh1, t1s, ds1)
-        da2 = self.t2.bwd(dh2, t2s, ds2)
-        self.d1.wgrad(da1, ctx2)
+        da1 = self.t1.bwd(dh1, t1s, ds1, dxsum=self.d1.gb)
+        da2 = self.t2.bwd(dh2, t2s, ds2, dxsum=self.d2.gb)
+        self.d1.wgrad(da1, ctx2, bias_done=True)
         dctx2 = self.d1.dgrad(da1)
-        self.d2.wgrad(da2, ctx1)
+        self.d2.wgrad(da2, ctx1, bias_done=True)
         dctx1 = self.d2.dgrad(da2)
         dq1 = torch.empty_like(q1)
         dq2 = torch.empty_like(q2)

@@ -69,7 +69,8 @@ def _splitk(m, n, k):
 
 
 def linear_wgrad(dy, x, gW, gb=None, alpha=1.0):
-    """gW += alpha * dy^T . x ; gb += alpha * colsum(dy).  dy [M,N], x [M,K], gW [N,K] fp32."""
+    """gW += alpha * dy^T . x ; gb += alpha * colsum(dy) (gb None: the bias gradient was fused into
+    dy's producer).  dy [M,N], x [M,K], gW [N,K] fp32."""
     M, N = dy.shape
     K = x.shape[1]
     s = _splitk(N, K, M)
@@ -103,12 +104,17 @@ def ln_fwd(x, res, gamma, beta, y, xhat, rstd, p_in=0.0, p_out=0.0, seed=0, off_
          p_out, seed, off_in, off_out, dt(x), stream())
 
 
+LN_BWD_SLABS = 512   # K3M_LN_BWD_SLABS (include/k3m_hip.h)
+
+
 def ln_bwd(dy, xhat, rstd, gamma, dres, dx, dgamma, dbeta, p_in=0.0, p_out=0.0, seed=0, off_in=0, off_out=0,
-           acc_res=False):
+           acc_res=False, dxsum=None):
+    """dxsum: optional fp32 [cols] that the column sums of dx are accumulated into (the bias
+    gradient of the Linear whose output fed this LayerNorm)."""
     rows, cols = dy.shape
-    ws = torch.empty((2 * 128 * cols,), dtype=torch.float32, device=dy.device)
-    call("k3m_ln_bwd", ptr(dy), ptr(xhat), ptr(rstd), ptr(gamma), ptr(dres), ptr(dx), ptr(dgamma), ptr(dbeta), rows,
-         cols, p_in, p_out, seed, off_in, off_out, int(acc_res), ptr(ws), dt(dy), stream())
+    ws = torch.empty((3 * LN_BWD_SLABS * cols,), dtype=torch.float32, device=dy.device)
+    call("k3m_ln_bwd", ptr(dy), ptr(xhat), ptr(rstd), ptr(gamma), ptr(dres), ptr(dx), ptr(dgamma), ptr(dbeta),
+         ptr(dxsum), rows, cols, p_in, p_out, seed, off_in, off_out, int(acc_res), ptr(ws), dt(dy), stream())
 
 
 def embed_fwd(ids, tt, word, pos, typ, gamma, beta, y0, y1, y2, xhat, rstd, p_out, seed, off, eps=1e-12):
@@ -133,6 +139,18 @@ def attn_bwd(dctx, o, q, k, v, probs, dq, dk, dv, nseq, lq, lk, nh, hd, scale, p
     call("k3m_attn_bwd", ptr(dctx), _ld(dctx), ptr(o), _ld(o), ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v), ptr(probs), ptr(dq),
          ptr(dk), ptr(dv), _ld(dq), _ld(dk), _ld(dv), nseq, lq, lk, nh, hd, scale, p_drop, seed, off, dt(dctx),
          stream())
+
+
+def flash_attn_fwd(q, k, v, kmask, ctx, lse, nseq, lq, lk, nh, hd, scale, p_drop, seed, off):
+    """bf16 attention forward saving the row log-sum-exp (lse: fp32 [nseq*nh*lq])."""
+    call("k3m_flash_attn_fwd", ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v), ptr(kmask), ptr(ctx), _ld(ctx),
+         ptr(lse), nseq, lq, lk, nh, hd, scale, p_drop, seed, off, stream())
+
+
+def flash_attn_bwd(dctx, o, q, k, v, kmask, lse, dq, dk, dv, nseq, lq, lk, nh, hd, scale, p_drop, seed, off):
+    call("k3m_flash_attn_bwd", ptr(dctx), _ld(dctx), ptr(o), _ld(o), ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v),
+         ptr(kmask), ptr(lse), ptr(dq), ptr(dk), ptr(dv), _ld(dq), _ld(dk), _ld(dv), nseq, lq, lk, nh, hd, scale,
+         p_drop, seed, off, stream())
 
 
 # ------------------------------------------------------------------ elementwise / rows

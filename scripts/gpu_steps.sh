@@ -24,11 +24,13 @@ for s in "$@"; do
     gpu) step gputests 1200 python -m pytest tests -m gpu -q ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
     benchq) step bench 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    profbf) export TMPDIR=/tmp; step profbf 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profbf -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --dtype bf16 ;;
     prof) export TMPDIR=/tmp; step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     gemm) step gemm 300 python scripts/gemm_bench.py all 10 both ;;
     gemmbf) step gemmbf 300 python scripts/gemm_bench.py all 10 bf16 ;;
     pbf) step pbf 900 python -m pytest tests/test_gpu_parity.py -q -s -k bf16 ;;
     benchbf) step benchbf 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --dtype bf16 ;;
+    attn) step attn 300 python scripts/attn_bench.py both ;;
     tbf) step tbf 600 python -m pytest tests/test_gpu_gemm_bf16.py -q ;;
     ddp2) step ddp2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --backend gloo --batch 16 ;;
     pmc) export TMPDIR=/tmp

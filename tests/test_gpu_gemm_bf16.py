@@ -169,3 +169,55 @@ def test_attention_bf16(dev, lq, lk, nh, hd):
     assert _rel(dq.view(B, lq, D), qr.grad) < 2e-2
     assert _rel(dk.view(B, lk, D), kr.grad) < 2e-2
     assert _rel(dv.view(B, lk, D), vr.grad) < 2.0 ** -6
+
+
+@pytest.mark.parametrize("lq,lk,nh,hd", [(36, 36, 12, 64), (128, 128, 12, 64), (37, 37, 8, 128), (36, 37, 8, 128),
+                                         (128, 37, 8, 128), (37, 128, 8, 128), (128, 36, 8, 128), (20, 90, 4, 64),
+                                         (1, 5, 2, 64)])
+def test_flash_attention_bf16(dev, lq, lk, nh, hd):
+    """LSE-saving bf16 attention (attention_bf16.hip) against fp32 math on the same bf16 inputs,
+    and, with dropout on, against the probability-saving kernel drawing the same mask."""
+    import math
+    from k3m_amd import ops
+    B, D = 5, nh * hd
+    g = torch.Generator(device="cpu").manual_seed(lq * 131 + lk)
+    qkv_q = torch.randn(B * lq, 3 * D, generator=g).to(dev).bfloat16()
+    qkv_k = torch.randn(B * lk, 3 * D, generator=g).to(dev).bfloat16()
+    q, k, v = qkv_q[:, :D], qkv_k[:, D:2 * D], qkv_k[:, 2 * D:]
+    m = torch.ones(B, lk, device=dev)
+    m[:, max(1, lk - 3):] = 0
+    mask = ((1 - m) * -10000).contiguous()
+    sc = 1 / math.sqrt(hd)
+    ctx = torch.empty(B * lq, D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * nh * lq, device=dev)
+    ops.flash_attn_fwd(q, k, v, mask, ctx, lse, B, lq, lk, nh, hd, sc, 0.0, 0, 0)
+    qr, kr, vr = [t.float().reshape(B, -1, D).clone().requires_grad_(True) for t in (q, k, v)]
+    qh = qr.view(B, lq, nh, hd).permute(0, 2, 1, 3)
+    kh = kr.view(B, lk, nh, hd).permute(0, 2, 1, 3)
+    vh = vr.view(B, lk, nh, hd).permute(0, 2, 1, 3)
+    sco = qh @ kh.transpose(-1, -2) * sc + mask[:, None, None, :]
+    p = torch.softmax(sco, -1)
+    cr = (p @ vh).permute(0, 2, 1, 3).reshape(B, lq, D)
+    assert _rel(lse.view(B, nh, lq), torch.logsumexp(sco, -1)) < 1e-4
+    assert _rel(ctx.view(B, lq, D), cr) < 2e-2
+    dctx = torch.randn(B * lq, D, generator=g).to(dev).bfloat16()
+    cr.backward(dctx.float().view(B, lq, D))
+    dq, dk, dv = [torch.empty(B * n_, D, device=dev, dtype=torch.bfloat16) for n_ in (lq, lk, lk)]
+    ops.flash_attn_bwd(dctx, ctx, q, k, v, mask, lse, dq, dk, dv, B, lq, lk, nh, hd, sc, 0.0, 0, 0)
+    # P and dS are rounded to bf16 before the dV / dK products (the rest is fp32-accumulated)
+    assert _rel(dq.view(B, lq, D), qr.grad) < 3e-2
+    assert _rel(dk.view(B, lk, D), kr.grad) < 3e-2
+    assert _rel(dv.view(B, lk, D), vr.grad) < 2e-2
+    # dropout: same counter-based mask as the probability-saving kernel
+    c1 = torch.empty_like(ctx)
+    c2 = torch.empty_like(ctx)
+    probs = torch.empty(B * nh * lq * lk, device=dev)
+    ops.flash_attn_fwd(q, k, v, mask, c1, lse, B, lq, lk, nh, hd, sc, 0.1, 11, 5)
+    ops.attn_fwd(q, k, v, mask, c2, probs, B, lq, lk, nh, hd, sc, 0.1, 11, 5)
+    assert _rel(c1, c2) < 2e-2
+    g1 = [torch.empty_like(t) for t in (dq, dk, dv)]
+    g2 = [torch.empty_like(t) for t in (dq, dk, dv)]
+    ops.flash_attn_bwd(dctx, c1, q, k, v, mask, lse, *g1, B, lq, lk, nh, hd, sc, 0.1, 11, 5)
+    ops.attn_bwd(dctx, c2, q, k, v, probs, *g2, B, lq, lk, nh, hd, sc, 0.1, 11, 5)
+    for a, b in zip(g1, g2):
+        assert _rel(a, b) < 4e-2

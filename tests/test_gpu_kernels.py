@@ -111,10 +111,12 @@ def test_layernorm(dev, cols):
     dres = torch.empty_like(x)
     dg = torch.zeros(cols, device=dev)
     db = torch.zeros(cols, device=dev)
-    ops.ln_bwd(dy, xh, rs, g, dres, dres, dg, db)
+    xs = torch.ones(cols, device=dev)
+    ops.ln_bwd(dy, xh, rs, g, dres, dres, dg, db, dxsum=xs)
     assert _rel(dres, xr.grad) < 1e-4
     assert _rel(dg, gr.grad) < 1e-4
     assert _rel(db, br.grad) < 1e-4
+    assert _rel(xs, 1 + xr.grad.sum(0)) < 1e-4   # fused bias gradient of the producing Linear
 
 
 def test_dropout_ln_regenerates_mask(dev):
@@ -128,7 +130,9 @@ def test_dropout_ln_regenerates_mask(dev):
     ops.ln_fwd(x, None, g, b, y, xh, rs, p_in=0.1, seed=5, off_in=77)
     dx, dres = torch.empty_like(x), torch.empty_like(x)
     dg, db = torch.zeros(cols, device=dev), torch.zeros(cols, device=dev)
-    ops.ln_bwd(torch.randn_like(x), xh, rs, g, dres, dx, dg, db, p_in=0.1, seed=5, off_in=77)
+    xs = torch.zeros(cols, device=dev)
+    ops.ln_bwd(torch.randn_like(x), xh, rs, g, dres, dx, dg, db, p_in=0.1, seed=5, off_in=77, dxsum=xs)
+    assert _rel(xs, dx.sum(0)) < 1e-4
     frac = float((dx == 0).float().mean())
     assert 0.08 < frac < 0.12
     ratio = dx[dx != 0] / dres[dx != 0]
