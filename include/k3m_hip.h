@@ -111,7 +111,7 @@ int k3m_attn_bwd(const void* dctx, long long ldc, const void* o, long long ldo, 
                  float scale, float p_drop, uint64_t seed, uint64_t off, int dtype, hipStream_t stream);
 
 /* bf16 attention for the mixed-precision encoder (same semantics as k3m_attn_fwd/bwd; head dim
- * 64 or 128, L <= 128): instead of the [nseq, nh, lq, lk] probabilities the forward saves the row
+ * 64, 96 or 128, L <= 128): instead of the [nseq, nh, lq, lk] probabilities the forward saves the row
  * log-sum-exp lse [nseq, nh, lq] and the backward recomputes P from it (kmask is needed again).
  * Every row pointer + ld must allow 16-byte loads (ld % 8 == 0, 16-B aligned base). */
 int k3m_flash_attn_fwd(const void* q, long long ldq, const void* k, long long ldk, const void* v, long long ldv,

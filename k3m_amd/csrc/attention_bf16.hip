@@ -1,4 +1,4 @@
-// bf16 fused attention for the short K3M sequences (L <= 128, head dim 64 or 128) on
+// bf16 fused attention for the short K3M sequences (L <= 128, head dim 64, 96 or 128) on
 // v_mfma_f32_32x32x16_bf16 — the mixed-precision encoder's attention.
 //
 // One workgroup (4 waves) per (sequence, head); Q, K, V (and dO) live in LDS as bf16 row-major
@@ -78,9 +78,10 @@ __device__ __forceinline__ floatx16 zero16() {
 
 // stage rows [row0, row0 + nrows) x [coff, coff + 8 NC) of a bf16 matrix into an image
 // (rows >= nvalid zero); all loads issued before the LDS writes
-template <int NC>
+template <int NC, int NCI>
 __device__ __forceinline__ void stage(uint16_t* img, const uint16_t* __restrict__ src, long long row0, long long ld,
                                       int coff, int nrows, int nvalid) {
+  // NC chunks per source row, written into an image laid out with NCI chunks per row
   constexpr int U = MAXL * NC / NT;
   uint4 r[U];
 #pragma unroll
@@ -94,7 +95,7 @@ __device__ __forceinline__ void stage(uint16_t* img, const uint16_t* __restrict_
   for (int u = 0; u < U; ++u) {
     const int e = threadIdx.x + u * NT;
     const int i = e / NC, c = e % NC;
-    if (i < nrows) *reinterpret_cast<uint4*>(img + ioff<NC>(i, c)) = r[u];
+    if (i < nrows) *reinterpret_cast<uint4*>(img + ioff<NCI>(i, c)) = r[u];
   }
 }
 
@@ -107,21 +108,23 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __rest
                                                           long long ldc, float* __restrict__ lse, int lq, int lk,
                                                           int nh, float scale, float p_drop, uint64_t seed,
                                                           uint64_t off) {
-  constexpr int NC = HD / 8, DT = HD / 32, KS = HD / 16;
+  // head dim 96 rows are stored 128 wide (the 16-chunk swizzle) and only 12 chunks are used
+  constexpr int NCL = HD / 8, NC = HD == 96 ? 16 : HD / 8, DT = HD / 32, KS = HD / 16;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int s = blockIdx.x / nh, h = blockIdx.x % nh;
   const int LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
   uint16_t* Qs = smem;
-  uint16_t* Ks = Qs + LQ * HD;
-  uint16_t* Vs = Ks + LK * HD;
-  float* msk = reinterpret_cast<float*>(Vs + LK * HD);
+  constexpr int HW = NC * 8;   // image row width
+  uint16_t* Ks = Qs + LQ * HW;
+  uint16_t* Vs = Ks + LK * HW;
+  float* msk = reinterpret_cast<float*>(Vs + LK * HW);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
   const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
   const int hoff = h * HD;
 
-  stage<NC>(Qs, q, qrow0, ldq, hoff, LQ, lq);
-  stage<NC>(Ks, k, krow0, ldk, hoff, LK, lk);
-  stage<NC>(Vs, v, krow0, ldv, hoff, LK, lk);
+  stage<NCL, NC>(Qs, q, qrow0, ldq, hoff, LQ, lq);
+  stage<NCL, NC>(Ks, k, krow0, ldk, hoff, LK, lk);
+  stage<NCL, NC>(Vs, v, krow0, ldv, hoff, LK, lk);
   for (int j = threadIdx.x; j < LK; j += NT) msk[j] = j < lk ? (kmask ? kmask[krow0 + j] : 0.f) : -INFINITY;
   __syncthreads();
   const int i0 = 32 * w;
@@ -214,16 +217,18 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kernel(const uint16_t* __rest
                                                           uint16_t* __restrict__ dv, long long lddq, long long lddk,
                                                           long long lddv, int lq, int lk, int nh, float scale,
                                                           float p_drop, uint64_t seed, uint64_t off) {
-  constexpr int NC = HD / 8, DT = HD / 32, KS = HD / 16;
+  // head dim 96 rows are stored 128 wide (the 16-chunk swizzle) and only 12 chunks are used
+  constexpr int NCL = HD / 8, NC = HD == 96 ? 16 : HD / 8, DT = HD / 32, KS = HD / 16;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int s = blockIdx.x / nh, h = blockIdx.x % nh;
   const int LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
   const int PW = LK == 96 ? 128 : LK;          // row width of the P / dS images (NC 4, 8 or 16)
   uint16_t* Qs = smem;
-  uint16_t* dOs = Qs + LQ * HD;
-  uint16_t* Ks = dOs + LQ * HD;
-  uint16_t* Vs = Ks + LK * HD;
-  uint16_t* Ps = Vs + LK * HD;                 // [LQ][PW] P_drop
+  constexpr int HW = NC * 8;   // image row width
+  uint16_t* dOs = Qs + LQ * HW;
+  uint16_t* Ks = dOs + LQ * HW;
+  uint16_t* Vs = Ks + LK * HW;
+  uint16_t* Ps = Vs + LK * HW;                 // [LQ][PW] P_drop
   uint16_t* dSs = Ps + LQ * PW;                // [LQ][PW] dS
   float* msk = reinterpret_cast<float*>(dSs + LQ * PW);
   float* Ls = msk + LK;
@@ -233,10 +238,10 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kernel(const uint16_t* __rest
   const int hoff = h * HD;
   const long long lrow0 = ((long long)s * nh + h) * lq;
 
-  stage<NC>(Qs, q, qrow0, ldq, hoff, LQ, lq);
-  stage<NC>(dOs, dctx, qrow0, ldc, hoff, LQ, lq);
-  stage<NC>(Ks, k, krow0, ldk, hoff, LK, lk);
-  stage<NC>(Vs, v, krow0, ldv, hoff, LK, lk);
+  stage<NCL, NC>(Qs, q, qrow0, ldq, hoff, LQ, lq);
+  stage<NCL, NC>(dOs, dctx, qrow0, ldc, hoff, LQ, lq);
+  stage<NCL, NC>(Ks, k, krow0, ldk, hoff, LK, lk);
+  stage<NCL, NC>(Vs, v, krow0, ldv, hoff, LK, lk);
   for (int j = threadIdx.x; j < LK; j += NT) msk[j] = j < lk ? (kmask ? kmask[krow0 + j] : 0.f) : -INFINITY;
   {
     // D_i = dO_i . O_i: two threads per row, each over half of the head dimension (16-B loads)
@@ -375,10 +380,12 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kernel(const uint16_t* __rest
 
 size_t fwd_lds(int lq, int lk, int hd) {
   const size_t LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
+  if (hd == 96) hd = 128;
   return 2 * (LQ * hd + 2 * LK * hd) + 4 * LK;
 }
 size_t bwd_lds(int lq, int lk, int hd) {
   const size_t LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
+  if (hd == 96) hd = 128;
   const size_t PW = LK == 96 ? 128 : LK;
   return 2 * (2 * LQ * hd + 2 * LK * hd + 2 * LQ * PW) + 4 * (LK + 2 * LQ);
 }
@@ -390,6 +397,8 @@ void set_attrs() {
   if (!done) {
     (void)hipFuncSetAttribute((const void*)flash_fwd_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_fwd_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_fwd_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_bwd_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_bwd_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_bwd_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     done = true;
@@ -405,13 +414,18 @@ extern "C" int k3m_flash_attn_fwd(const void* q, long long ldq, const void* k, l
                                   int lq, int lk, int nh, int hd, float scale, float p_drop, uint64_t seed,
                                   uint64_t off, hipStream_t st) {
   K3M_ARG(q && k && v && ctx && lse);
-  K3M_ARG(lq > 0 && lq <= MAXL && lk > 0 && lk <= MAXL && (hd == 64 || hd == 128) && nh > 0 && nseq >= 0);
+  K3M_ARG(lq > 0 && lq <= MAXL && lk > 0 && lk <= MAXL && (hd == 64 || hd == 96 || hd == 128) && nh > 0 && nseq >= 0);
   K3M_ARG(vec_ok(q, ldq) && vec_ok(k, ldk) && vec_ok(v, ldv));
   if (nseq == 0) return 0;
   const size_t lds = fwd_lds(lq, lk, hd);
   K3M_ARG(lds <= (size_t)LDS_MAX);
   set_attrs();
-  if (hd == 64)
+#define K3M_FLASH_FWD(HD_)                                                                                       \
+  hipLaunchKernelGGL(flash_fwd_kernel<HD_>, dim3(nseq * nh), dim3(NT), lds, st, (const uint16_t*)q, ldq,            \
+                     (const uint16_t*)k, ldk, (const uint16_t*)v, ldv, kmask, (uint16_t*)ctx, ldc, lse, lq, lk, nh, \
+                     scale, p_drop, seed, off)
+  if (hd == 96) K3M_FLASH_FWD(96);
+  else if (hd == 64)
     hipLaunchKernelGGL(flash_fwd_kernel<64>, dim3(nseq * nh), dim3(NT), lds, st, (const uint16_t*)q, ldq,
                        (const uint16_t*)k, ldk, (const uint16_t*)v, ldv, kmask, (uint16_t*)ctx, ldc, lse, lq, lk, nh,
                        scale, p_drop, seed, off);
@@ -429,13 +443,18 @@ extern "C" int k3m_flash_attn_bwd(const void* dctx, long long ldc, const void* o
                                   long long lddk, long long lddv, int nseq, int lq, int lk, int nh, int hd,
                                   float scale, float p_drop, uint64_t seed, uint64_t off, hipStream_t st) {
   K3M_ARG(dctx && o && q && k && v && lse && dq && dk && dv);
-  K3M_ARG(lq > 0 && lq <= MAXL && lk > 0 && lk <= MAXL && (hd == 64 || hd == 128) && nh > 0 && nseq >= 0);
+  K3M_ARG(lq > 0 && lq <= MAXL && lk > 0 && lk <= MAXL && (hd == 64 || hd == 96 || hd == 128) && nh > 0 && nseq >= 0);
   K3M_ARG(vec_ok(q, ldq) && vec_ok(k, ldk) && vec_ok(v, ldv) && vec_ok(dctx, ldc) && vec_ok(o, ldo));
   if (nseq == 0) return 0;
   const size_t lds = bwd_lds(lq, lk, hd);
   K3M_ARG(lds <= (size_t)LDS_MAX);
   set_attrs();
-  if (hd == 64)
+  if (hd == 96)
+    hipLaunchKernelGGL(flash_bwd_kernel<96>, dim3(nseq * nh), dim3(NT), lds, st, (const uint16_t*)dctx, ldc,
+                       (const uint16_t*)o, ldo, (const uint16_t*)q, ldq, (const uint16_t*)k, ldk, (const uint16_t*)v,
+                       ldv, kmask, lse, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, lddq, lddk, lddv, lq, lk, nh,
+                       scale, p_drop, seed, off);
+  else if (hd == 64)
     hipLaunchKernelGGL(flash_bwd_kernel<64>, dim3(nseq * nh), dim3(NT), lds, st, (const uint16_t*)dctx, ldc,
                        (const uint16_t*)o, ldo, (const uint16_t*)q, ldq, (const uint16_t*)k, ldk, (const uint16_t*)v,
                        ldv, kmask, lse, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, lddq, lddk, lddv, lq, lk, nh,

@@ -191,7 +191,7 @@ class FFN(object):
 
 def _flash(q, hd):
     # bf16 encoder: the LSE-saving bf16 kernels (attention_bf16.hip); fp32: exact-fp32 kernels
-    return q.dtype == torch.bfloat16 and hd in (64, 128)
+    return q.dtype == torch.bfloat16 and hd in (64, 96, 128)
 
 
 def _attn_fwd(q, k, v, mask, nseq, lq, lk, nh, p, rng, out=None):

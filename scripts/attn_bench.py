@@ -18,6 +18,8 @@ SHAPES = [  # name, nseq, lq, lk, nh, hd
     ("co pv->img", B, 128, 37, 8, 128),
     ("co img->pv", B, 37, 128, 8, 128),
     ("co pv->txt", B, 128, 36, 8, 128),
+    ("co2 pv->txt", B, 128, 36, 8, 96),
+    ("co2 txt->pv", B, 36, 128, 8, 96),
 ]
 
 
@@ -36,7 +38,7 @@ def run(name, nseq, lq, lk, nh, hd, dtype, reps=20):
     dv = torch.empty(nseq * lk, D, device=dev, dtype=dtype)
     sc = 1 / math.sqrt(hd)
 
-    flash = dtype == torch.bfloat16 and hd in (64, 128) and FLASH
+    flash = dtype == torch.bfloat16 and hd in (64, 96, 128) and FLASH
     lse = torch.empty(nseq * nh * lq, device=dev)
 
     def fwd():
