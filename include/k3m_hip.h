@@ -62,7 +62,7 @@ typedef struct K3mGemm {
 int k3m_gemm(const K3mGemm* g, hipStream_t stream);
 
 /* out[c] (+)= sum_r x[r*ld + c]  — bias gradients (autograd of every Linear bias).
- * ws: >= 256*cols floats. */
+ * ws: >= (256 + 16)*cols floats. */
 int k3m_colsum(const void* x, long long ld, int rows, int cols, float* out, int accumulate, float* ws,
                int dtype, hipStream_t stream);
 
@@ -77,7 +77,7 @@ int k3m_ln_fwd(const void* x, const void* res, const float* gamma, const float* 
  * accumulate_res), dx = dropout_in'(ds) is written to dx (may alias dres when p_in == 0).
  * dgamma/dbeta are ACCUMULATED (fp32 grad buffer).  dxsum (nullable): the column sums of dx are
  * ACCUMULATED into it — the bias gradient of the Linear that produced x, fused here instead of a
- * separate reduction over dx.  ws: >= 3*K3M_LN_BWD_SLABS*cols floats. */
+ * separate reduction over dx.  ws: >= 3*(K3M_LN_BWD_SLABS + 16)*cols floats. */
 #define K3M_LN_BWD_SLABS 512
 int k3m_ln_bwd(const void* dy, const void* xhat, const float* rstd, const float* gamma, void* dres, void* dx,
                float* dgamma, float* dbeta, float* dxsum, int rows, int cols, float p_in, float p_out, uint64_t seed,

@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
                                                      int rows, int cols, float p_in, float p_out, uint64_t seed,
                                                      uint64_t off_in, uint64_t off_out, int acc_res, int want_sum) {
   // column partials of dgamma, dbeta and (want_sum) sum(dx): per wave in registers, then one
-  // [3][cols] slab per block through LDS (reduced by slab_sum_kernel)
+  // [3][cols] slab per block through LDS (reduced by slab_reduce)
   __shared__ float red[4][1024];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nv = cols >> 8;
@@ -182,23 +182,52 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   }
 }
 
-// out[c] (+)= sum_k ws[k][c]: 32 columns x 8 partial sums per workgroup (latency-bound otherwise)
-__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ ws, int nslab, int cols,
-                                                       float* __restrict__ out, int accumulate) {
-  __shared__ float part[8][33];
-  const int cx = threadIdx.x & 31, ky = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + cx;
+// out[c] (+)= sum_k ws[k][c] in two deterministic passes (a single pass has too few workgroups for
+// 512 slabs x 768 columns and is latency-bound): slab_part sums groups of slabs into part[g][c]
+// (64 columns x 4 slab phases per workgroup), slab_final adds the <= 16 group partials.
+constexpr int SLAB_GROUPS = 16;
+struct SlabOut {   // up to 3 reductions of the same shape in one pair of launches
+  float* out[3];
+};
+__global__ __launch_bounds__(256) void slab_part_kernel(const float* __restrict__ ws, int nslab, int cols,
+                                                        float* __restrict__ part) {
+  // blockIdx.z selects the array: ws + z*nslab*cols -> part + z*gridDim.y*cols
+  __shared__ float red[4][64];
+  const int cx = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cx;
+  const float* src = ws + (long long)blockIdx.z * nslab * cols;
+  const int per = (nslab + gridDim.y - 1) / gridDim.y;
+  const int k0 = blockIdx.y * per, k1 = min(nslab, k0 + per);
   float s = 0.f;
   if (c < cols)
-    for (int k = ky; k < nslab; k += 8) s += ws[(long long)k * cols + c];
-  part[ky][cx] = s;
+    for (int k = k0 + ph; k < k1; k += 4) s += src[(long long)k * cols + c];
+  red[ph][cx] = s;
   __syncthreads();
-  if (ky == 0 && c < cols) {
-    float t = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) t += part[k][cx];
-    out[c] = accumulate ? out[c] + t : t;
-  }
+  if (ph == 0 && c < cols)
+    part[((long long)blockIdx.z * gridDim.y + blockIdx.y) * cols + c] = red[0][cx] + red[1][cx] + red[2][cx] + red[3][cx];
+}
+__global__ __launch_bounds__(256) void slab_final_kernel(const float* __restrict__ part, int ngroups, int cols,
+                                                         SlabOut outs, int accumulate) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  const float* p = part + (long long)blockIdx.y * ngroups * cols;
+  float t = 0.f;
+  for (int g = 0; g < ngroups; ++g) t += p[(long long)g * cols + c];
+  float* out = outs.out[blockIdx.y];
+  out[c] = accumulate ? out[c] + t : t;
+}
+// out_a[c] (+)= sum_k ws[a][k][c] for a < narr (arrays nslab*cols apart); part >= narr*16*cols floats
+void slab_reduce(const float* ws, int nslab, int cols, SlabOut outs, int narr, int accumulate, float* part,
+                 hipStream_t st) {
+  const int groups = std::max(1, std::min(SLAB_GROUPS, k3m_cdiv(nslab, 32)));
+  hipLaunchKernelGGL(slab_part_kernel, dim3(k3m_cdiv(cols, 64), groups, narr), dim3(256), 0, st, ws, nslab, cols,
+                     part);
+  hipLaunchKernelGGL(slab_final_kernel, dim3(k3m_cdiv(cols, 256), narr), dim3(256), 0, st, part, groups, cols, outs,
+                     accumulate);
+}
+void slab_reduce(const float* ws, int nslab, int cols, float* out, int accumulate, float* part, hipStream_t st) {
+  SlabOut o = {{out, nullptr, nullptr}};
+  slab_reduce(ws, nslab, cols, o, 1, accumulate, part, st);
 }
 
 // ------------------------------------------------------------------ embeddings
@@ -285,6 +314,62 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, lo
   ws[(long long)blockIdx.y * cols + c] = s;
 }
 
+// 16-byte vector form: 64 column groups of 8 x 4 row phases per workgroup, 512 columns per block
+template <typename T>
+__device__ __forceinline__ void load8f(const T* p, float (&v)[8]);
+template <>
+__device__ __forceinline__ void load8f<float>(const float* p, float (&v)[8]) {
+  const floatx4 a = *reinterpret_cast<const floatx4*>(p), b = *reinterpret_cast<const floatx4*>(p + 4);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[q] = a[q];
+    v[4 + q] = b[q];
+  }
+}
+template <>
+__device__ __forceinline__ void load8f<bf16_t>(const bf16_t* p, float (&v)[8]) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[2 * q] = __uint_as_float(w[q] << 16);
+    v[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+  }
+}
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_vec_kernel(const T* __restrict__ x, long long ld, int rows, int cols,
+                                                         float* __restrict__ ws) {
+  __shared__ float red[4][512];
+  const int cg = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int c = blockIdx.x * 512 + cg * 8;
+  const int chunk = (rows + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * chunk, r1 = min(rows, r0 + chunk);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < cols) {
+    int r = r0 + ph;
+    for (; r + 4 < r1; r += 8) {   // two rows in flight per thread
+      float a[8], b[8];
+      load8f<T>(x + (long long)r * ld + c, a);
+      load8f<T>(x + (long long)(r + 4) * ld + c, b);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s[q] += a[q] + b[q];
+    }
+    if (r < r1) {
+      float a[8];
+      load8f<T>(x + (long long)r * ld + c, a);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s[q] += a[q];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) red[ph][cg * 8 + q] = s[q];
+  __syncthreads();
+  for (int k = threadIdx.x; k < 512; k += 256) {
+    const int cc = blockIdx.x * 512 + k;
+    if (cc < cols) ws[(long long)blockIdx.y * cols + cc] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+  }
+}
+
 // ------------------------------------------------------------------ elementwise
 template <typename T>
 __global__ void dgelu_kernel(const T* g, const T* pre, T* out, long long n) {
@@ -364,12 +449,9 @@ extern "C" int k3m_ln_bwd(const void* dy, const void* xhat, const float* rstd, c
                                        gamma, (T*)dres, (T*)dx, ws, rows, cols, p_in, p_out, seed, off_in, off_out,
                                        acc_res, dxsum != nullptr));
   K3M_CHECK_LAUNCH();
-  hipLaunchKernelGGL(slab_sum_kernel, dim3(k3m_cdiv(cols, 32)), dim3(256), 0, st, ws, nb, cols, dgamma, 1);
-  hipLaunchKernelGGL(slab_sum_kernel, dim3(k3m_cdiv(cols, 32)), dim3(256), 0, st, ws + (long long)nb * cols, nb, cols,
-                     dbeta, 1);
-  if (dxsum)
-    hipLaunchKernelGGL(slab_sum_kernel, dim3(k3m_cdiv(cols, 32)), dim3(256), 0, st, ws + 2LL * nb * cols, nb, cols,
-                       dxsum, 1);
+  float* part = ws + 3LL * LN_BWD_BLOCKS * cols;
+  SlabOut outs = {{dgamma, dbeta, dxsum}};
+  slab_reduce(ws, nb, cols, outs, dxsum ? 3 : 2, 1, part, st);
   K3M_CHECK_LAUNCH();
   return 0;
 }
@@ -404,10 +486,16 @@ extern "C" int k3m_colsum(const void* x, long long ld, int rows, int cols, float
                           int dtype, hipStream_t st) {
   K3M_ARG(x && out && ws && rows >= 0 && cols >= 0);
   if (cols == 0) return 0;
-  const int chunks = std::max(1, std::min(K3M_COLSUM_SLABS, k3m_cdiv(rows, 32)));
-  DISPATCH_T(dtype, hipLaunchKernelGGL(colsum_kernel<T>, dim3(k3m_cdiv(cols, 256), chunks), dim3(256), 0, st,
-                                       (const T*)x, ld, rows, cols, ws));
-  hipLaunchKernelGGL(slab_sum_kernel, dim3(k3m_cdiv(cols, 32)), dim3(256), 0, st, ws, chunks, cols, out, accumulate);
+  const int chunks = std::max(1, std::min(K3M_COLSUM_SLABS, k3m_cdiv(rows, 64)));
+  const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && ld % 8 == 0 && cols % 8 == 0;
+  if (vec) {
+    DISPATCH_T(dtype, hipLaunchKernelGGL(colsum_vec_kernel<T>, dim3(k3m_cdiv(cols, 512), chunks), dim3(256), 0, st,
+                                         (const T*)x, ld, rows, cols, ws));
+  } else {
+    DISPATCH_T(dtype, hipLaunchKernelGGL(colsum_kernel<T>, dim3(k3m_cdiv(cols, 256), chunks), dim3(256), 0, st,
+                                         (const T*)x, ld, rows, cols, ws));
+  }
+  slab_reduce(ws, chunks, cols, out, accumulate, ws + (long long)K3M_COLSUM_SLABS * cols, st);
   K3M_CHECK_LAUNCH();
   return 0;
 }

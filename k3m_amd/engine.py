@@ -86,6 +86,11 @@ class FlatParams(object):
             self.p[name].copy_(t.to(torch.float32).reshape(self.shapes[name]))
         self.shadow_fresh = False
 
+    def p16(self, name):
+        """bf16 shadow view of one parameter (bf16 mode only)."""
+        o = self.offsets[name]
+        return self.data16[o:o + math.prod(self.shapes[name])].view(self.shapes[name])
+
     def refresh_shadow(self):
         """bf16 shadow <- fp32 parameters (after loads / external optimizers; the Trainer's AdamW
         writes the shadow itself)."""
@@ -117,8 +122,9 @@ class Lin(object):
         # operands share a dtype: a bf16 activation multiplies the bf16 weight shadow
         return self.W16 if x.dtype == torch.bfloat16 else self.W
 
-    def fwd(self, x, out=None, epi=None, aux=None, alpha=1.0, beta=0.0):
-        return ops.linear(x, self._w(x), self.b, out=out, epi=epi, aux=aux, alpha=alpha, beta=beta)
+    def fwd(self, x, out=None, epi=None, aux=None, alpha=1.0, beta=0.0, out_dtype=None):
+        return ops.linear(x, self._w(x), self.b, out=out, epi=epi, aux=aux, alpha=alpha, beta=beta,
+                          out_dtype=out_dtype)
 
     def wgrad(self, dy, x, alpha=1.0, bias_done=False):
         """bias_done: the bias gradient was already accumulated by dy's producer (k3m_ln_bwd dxsum)."""
@@ -372,6 +378,13 @@ class K3MEngine(object):
         self.sw1, self.sw3 = Lin(fp, "struc_w1"), Lin(fp, "struc_w3")
         self.schedule = self._schedule()
 
+    def _lo(self, x):
+        """bf16 operand copy of an fp32 activation for the large fp32-region GEMMs (fusion gates, tied
+        MLM decoder) in bf16 mode; the activation itself stays fp32.  Identity in fp32 mode."""
+        if self.dtype != "bf16":
+            return x
+        return ops.convert(x.contiguous(), torch.empty(x.shape, dtype=torch.bfloat16, device=x.device))
+
     # ------------------------------------------------------------ encoder schedule
     def _schedule(self):
         """[(kind, index)] in lock-step order: ('t', i) text layer on all four text/PV streams,
@@ -505,7 +518,7 @@ class K3MEngine(object):
                 cc = torch.empty((rows, 3 * D), dtype=torch.float32, device=dev)
                 L.call("k3m_relu_cat3", x0.data_ptr(), x1.data_ptr(), x2.data_ptr(), cc.data_ptr(), rows, D, L.F32,
                        L.stream())
-                a = self.gate[m].fwd(cc, epi=L.EPI_BIAS_SIGMOID)
+                a = self.gate[m].fwd(self._lo(cc), epi=L.EPI_BIAS_SIGMOID, out_dtype=torch.float32)
                 ys = torch.empty_like(a)
                 idx = torch.empty((rows * D,), dtype=torch.uint8, device=dev)
                 nz = None
@@ -605,8 +618,9 @@ class K3MEngine(object):
         rs_m = torch.empty((n_m,), dtype=torch.float32, device=dev)
         if n_m:
             ops.ln_fwd(hm1, None, self.mlm_ln.g, self.mlm_ln.b, hl, xh_m, rs_m)
-        E = fp.p["embeddings.word_embeddings.weight"]
-        logits = ops.linear(hl, E, fp.p["cls.predictions.bias"])
+        E = fp.p["embeddings.word_embeddings.weight"] if self.dtype != "bf16" else fp.p16(
+            "embeddings.word_embeddings.weight")
+        logits = ops.linear(self._lo(hl), E, fp.p["cls.predictions.bias"], out_dtype=torch.float32)
         lr_m = torch.empty((n_m,), dtype=torch.float32, device=dev)
         L.call("k3m_ce_fwd_bwd", logits.data_ptr(), V, lab_m.data_ptr(), sc_m.data_ptr(), n_m, V, lr_m.data_ptr(),
                L.stream())
@@ -670,10 +684,13 @@ class K3MEngine(object):
         # ---- MLM head (dlogits already in place from the forward CE kernel)
         idx_m, n_m, hm, pre_m, hl, xh_m, rs_m, dlog = ctx["mlm"]
         if n_m:
-            E = fp.p["embeddings.word_embeddings.weight"]
+            bf = self.dtype == "bf16"
+            E = fp.p16("embeddings.word_embeddings.weight") if bf else fp.p["embeddings.word_embeddings.weight"]
             gE = fp.g["embeddings.word_embeddings.weight"]
-            dhl = ops.linear_dgrad(dlog, E, alpha=w_mlm)
-            ops.linear_wgrad(dlog, hl, gE, fp.g["cls.predictions.bias"], alpha=w_mlm)
+            dlo = self._lo(dlog)
+            dhl = ops.linear_dgrad(dlo, E, dx=torch.empty(hl.shape, dtype=torch.float32, device=dev), alpha=w_mlm)
+            ops.linear_wgrad(dlo, self._lo(hl), gE, None, alpha=w_mlm)
+            ops.colsum(dlog, fp.g["cls.predictions.bias"], accumulate=True, alpha=w_mlm)
             dh1 = torch.empty_like(hl)
             ops.ln_bwd(dhl, xh_m, rs_m, self.mlm_ln.g, dh1, dh1, self.mlm_ln.gg, self.mlm_ln.gb)
             du = torch.empty_like(hl)
@@ -755,8 +772,10 @@ class K3MEngine(object):
                 dpre = torch.empty_like(cc)
                 L.call("k3m_gate_bwd", dout.data_ptr(), a.data_ptr(), cc.data_ptr(), ys.data_ptr(), idx.data_ptr(),
                        dc.data_ptr(), dpre.data_ptr(), rows, D, L.F32, L.stream())
-                self.gate[m].dgrad(dpre, dx=dc, beta=1.0)
-                self.gate[m].wgrad(dpre, cc)
+                dlo = self._lo(dpre)
+                self.gate[m].dgrad(dlo, dx=dc, beta=1.0)
+                self.gate[m].wgrad(dlo, self._lo(cc), bias_done=True)
+                ops.colsum(dpre, self.gate[m].gb, accumulate=True)
                 L.call("k3m_relu_split3_bwd", dc.data_ptr(), cc.data_ptr(), d0.data_ptr(), d1.data_ptr(), d2.data_ptr(),
                        rows, D, 0, L.F32, L.stream())
             else:

@@ -39,12 +39,12 @@ def gemm(a, a_trans, b, b_trans, c, m, n, k, epi=L.EPI_NONE, bias=None, aux=None
     return c
 
 
-def linear(x, W, b=None, out=None, epi=None, aux=None, alpha=1.0, beta=0.0):
+def linear(x, W, b=None, out=None, epi=None, aux=None, alpha=1.0, beta=0.0, out_dtype=None):
     """out = x . W^T (+ b) with epilogue; x [M,K] (row view), W [N,K]."""
     M, K = x.shape
     N = W.shape[0]
     if out is None:
-        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+        out = torch.empty((M, N), dtype=out_dtype or x.dtype, device=x.device)
     if epi is None:
         epi = L.EPI_BIAS if b is not None else L.EPI_NONE
     return gemm(x, 0, W, 1, out, M, N, K, epi, b, aux, alpha, beta)
@@ -82,7 +82,7 @@ def linear_wgrad(dy, x, gW, gb=None, alpha=1.0):
 
 def colsum(x, out, accumulate=True, alpha=1.0):
     rows, cols = x.shape
-    ws = torch.empty((256 * cols,), dtype=torch.float32, device=x.device)
+    ws = torch.empty(((256 + 16) * cols,), dtype=torch.float32, device=x.device)
     if alpha == 1.0:
         call("k3m_colsum", ptr(x), _ld(x), rows, cols, ptr(out), int(accumulate), ptr(ws), dt(x), stream())
     else:
@@ -112,7 +112,7 @@ def ln_bwd(dy, xhat, rstd, gamma, dres, dx, dgamma, dbeta, p_in=0.0, p_out=0.0, 
     """dxsum: optional fp32 [cols] that the column sums of dx are accumulated into (the bias
     gradient of the Linear whose output fed this LayerNorm)."""
     rows, cols = dy.shape
-    ws = torch.empty((3 * LN_BWD_SLABS * cols,), dtype=torch.float32, device=dy.device)
+    ws = torch.empty((3 * (LN_BWD_SLABS + 16) * cols,), dtype=torch.float32, device=dy.device)
     call("k3m_ln_bwd", ptr(dy), ptr(xhat), ptr(rstd), ptr(gamma), ptr(dres), ptr(dx), ptr(dgamma), ptr(dbeta),
          ptr(dxsum), rows, cols, p_in, p_out, seed, off_in, off_out, int(acc_res), ptr(ws), dt(dy), stream())
 

@@ -99,7 +99,7 @@ def test_train_mode_step_is_finite_and_learns(dev):
 BF16_LOSS_RTOL = 1e-2
 BF16_GRAD_COS = 0.98
 BF16_GRAD_NORM_RTOL = 3e-2
-BF16_GLOBAL_COS = 0.999
+BF16_GLOBAL_COS = 0.995
 
 
 @pytest.mark.parametrize("case", CASES)
