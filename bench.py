@@ -26,6 +26,7 @@ sys.path.insert(0, HERE)
 
 PEAK_F32_MFMA = 157.3e12      # MI355X f32 MFMA dense peak (MI355X_MICROARCH.md)
 PEAK_BF16_MFMA = 2.5e15
+PEAK_F32_X6 = PEAK_BF16_MFMA / 6   # fp32 GEMM as 6 bf16 MFMA partial products (gemm_x6_tile.h)
 REF_FLOPS_PER_SAMPLE = 319.31e9   # reference algorithmic fwd+bwd FLOPs/sample at config 2
 
 
@@ -85,7 +86,7 @@ def pmc_traffic(key, kernel_prefix):
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    if tuple(d.get("shape", ())) != tuple(key) or not d.get("kernel", "").startswith(kernel_prefix):
+    if tuple(d.get("shape", ())) != tuple(key) or kernel_prefix not in d.get("kernel", ""):
         return None
     return int(d["traffic_bytes"])
 
@@ -191,8 +192,10 @@ def main():
     gemm_flops = 2.0 * Mg * Ng * Kg
     achieved = gemm_flops / (gemm_ms * 1e-3) if gemm_ms else None
     bf = args.dtype == "bf16"
-    peak = PEAK_BF16_MFMA if bf else PEAK_F32_MFMA
-    kname = "gemm_bf16_kernel" if bf else "gemm_f32_kernel"
+    from k3m_amd import ops as _ops, _lib as _L
+    x6 = not bf and _ops.F32_ALGO == _L.F32_SPLIT_BF16X6
+    peak = PEAK_BF16_MFMA if bf else (PEAK_F32_X6 if x6 else PEAK_F32_MFMA)
+    kname = "gemm_bf16_kernel" if bf else ("gemm_x6_kernel" if x6 else "gemm_f32_kernel")
     res = {
         "metric": "pretrain samples/sec (whole job; bert_base_6layer_6conect, bs=64/GPU)",
         "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -211,7 +214,9 @@ def main():
                      "frac": round(achieved / peak, 4) if achieved else None,
                      "avg_launch_ms": round(gemm_ms, 4) if gemm_ms else None,
                      "launches": len(probe.events),
-                     "traffic": pmc_traffic(probe.key, "void (anonymous namespace)::" + kname),
+                     "peak_basis": ("bf16 dense MFMA" if bf else "fp32 via 6 bf16 MFMA partial products = bf16 dense peak / 6"
+                                    if x6 else "f32 MFMA"),
+                     "traffic": pmc_traffic(probe.key, kname),
                      "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/r1_gemm_ffn1_pmc.json)"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

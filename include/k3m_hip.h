@@ -28,6 +28,12 @@ extern "C" {
 
 enum K3mDType { K3M_F32 = 0, K3M_BF16 = 1 };
 
+/* How fp32-operand GEMMs use the matrix cores (accuracy: k3m_amd/csrc/gemm_x6_tile.h):
+ *   K3M_F32_SPLIT_BF16X6 — each fp32 operand split exactly into 3 bf16 planes, 6 bf16 MFMA partial
+ *                          products accumulated in fp32 (fp32-level accuracy, 416.7 TF/s roofline);
+ *   K3M_F32_MFMA_F32     — v_mfma_f32_32x32x2_f32 (exact f32 fma chain, 157.3 TF/s roofline). */
+enum K3mF32Algo { K3M_F32_SPLIT_BF16X6 = 0, K3M_F32_MFMA_F32 = 1 };
+
 enum K3mEpilogue {
   K3M_EPI_NONE = 0,         /* C = alpha*acc + beta*C                                        */
   K3M_EPI_BIAS = 1,         /* C = alpha*(acc + bias) + beta*C                               */
@@ -58,6 +64,7 @@ typedef struct K3mGemm {
   void* aux;
   float* ws;             /* splitk > 1: fp32 workspace of splitk*m*n floats (deterministic    */
   float alpha, beta;     /* slab reduction, no atomics)                                        */
+  int f32_algo;          /* fp32 operands: K3M_F32_SPLIT_BF16X6 (0, default) or K3M_F32_MFMA_F32 */
 } K3mGemm;
 int k3m_gemm(const K3mGemm* g, hipStream_t stream);
 

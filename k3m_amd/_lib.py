@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(_HERE, "libk3m_hip.so")
 
 F32, BF16 = 0, 1
 EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_DGELU, EPI_BIAS_SIGMOID = 0, 1, 2, 3, 4
+F32_SPLIT_BF16X6, F32_MFMA_F32 = 0, 1
 
 vp, i32, i64, f32, u64 = C.c_void_p, C.c_int, C.c_longlong, C.c_float, C.c_uint64
 
@@ -23,7 +24,7 @@ class K3mGemm(C.Structure):
     _fields_ = [("m", i32), ("n", i32), ("k", i32), ("a_trans", i32), ("b_trans", i32), ("epilogue", i32),
                 ("dtype", i32), ("splitk", i32), ("c_dtype", i32), ("lda", i64), ("ldb", i64), ("ldc", i64), ("ldaux", i64),
                 ("a", vp), ("b", vp), ("c", vp), ("bias", vp), ("aux", vp), ("ws", vp), ("alpha", f32),
-                ("beta", f32)]
+                ("beta", f32), ("f32_algo", i32)]
 
 
 # name -> argtypes (restype is always int status)

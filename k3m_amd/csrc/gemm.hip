@@ -1,14 +1,19 @@
 // MFMA GEMM entry point for gfx950 (k3m_gemm) and the fp32 tile policy.
 //
-// fp32 operands: the v_mfma_f32_32x32x2_f32 kernel of gemm_f32_tile.h (exact f32 products and
-// accumulation), tile chosen per shape:
+// fp32 operands, default (K3M_F32_SPLIT_BF16X6): the bf16x6 split kernel of gemm_x6_tile.h on the
+// bf16 matrix cores (fp32 accuracy, 2.67x the f32-MFMA roofline), tile chosen per shape:
+//   * 256x256x16 (8 waves, 1 block/CU) for the large forward / input-gradient GEMMs;
+//   * 128x128x32 (4 waves) for split-K weight gradients and mid-size grids;
+//   * 64x64x32 for the small co-attention GEMMs.
+// K3M_F32_MFMA_F32 (and unaligned operands): the v_mfma_f32_32x32x2_f32 kernel of gemm_f32_tile.h
+// (exact f32 products and accumulation), tile chosen per shape:
 //   * 256x256 (8 waves, 1 block/CU) when it still gives ~a block per CU: the fewest L2 bytes per FLOP;
 //   * 128x128 (4 waves, 2 blocks/CU) for split-K weight gradients and mid-size grids;
 //   * 64x128 / 64x64 for the small co-attention GEMMs (2,304-8,192 rows) that would otherwise leave
 //     CUs idle.
 // Split-K writes fp32 slabs (raw sums) reduced deterministically by splitk_reduce_kernel, which
 // applies alpha/beta.  bf16 operands go to gemm_bf16.hip.
-#include "gemm_f32_tile.h"
+#include "gemm_x6_tile.h"
 
 namespace {
 
@@ -65,6 +70,35 @@ int launch_tile_vec(const K3mGemm& g, bool ak, bool bk, hipStream_t st) {
   return launch_epi<TBM, TBN, WM, WN, OCC, false, true, true>(g, st);
 }
 
+template <int TBM, int TBN, int WM, int WN, int BK, int OCC, bool AK, bool BK_>
+int launch_x6_epi(const K3mGemm& g, hipStream_t st) {
+  const int tm = (g.m + TBM - 1) / TBM, tn = (g.n + TBN - 1) / TBN;
+  dim3 grid(tm * tn, g.splitk > 1 ? g.splitk : 1);
+  switch (g.epilogue) {
+#define K3M_GEMM_CASE(E)                                                                                          \
+    case E:                                                                                                       \
+      hipLaunchKernelGGL((k3m_x6::gemm_x6_kernel<TBM, TBN, WM, WN, BK, AK, BK_, true, E, OCC>), grid, dim3(64 * WM * WN), \
+                         0, st, g);                                                                               \
+      break;
+    K3M_GEMM_CASE(K3M_EPI_NONE)
+    K3M_GEMM_CASE(K3M_EPI_BIAS)
+    K3M_GEMM_CASE(K3M_EPI_BIAS_GELU)
+    K3M_GEMM_CASE(K3M_EPI_DGELU)
+    K3M_GEMM_CASE(K3M_EPI_BIAS_SIGMOID)
+#undef K3M_GEMM_CASE
+    default: return K3M_EINVAL;
+  }
+  return 0;
+}
+
+template <int TBM, int TBN, int WM, int WN, int BK, int OCC>
+int launch_x6(const K3mGemm& g, bool ak, bool bk, hipStream_t st) {
+  if (ak && bk) return launch_x6_epi<TBM, TBN, WM, WN, BK, OCC, true, true>(g, st);
+  if (ak) return launch_x6_epi<TBM, TBN, WM, WN, BK, OCC, true, false>(g, st);
+  if (bk) return launch_x6_epi<TBM, TBN, WM, WN, BK, OCC, false, true>(g, st);
+  return launch_x6_epi<TBM, TBN, WM, WN, BK, OCC, false, false>(g, st);
+}
+
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 long long nblocks(const K3mGemm& g, int bm, int bn) {
@@ -86,6 +120,7 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
   K3M_ARG(g.splitk <= 1 || (g.epilogue == K3M_EPI_NONE && g.ws));
   K3M_ARG(g.epilogue == K3M_EPI_NONE || g.epilogue == K3M_EPI_DGELU || g.bias);
   K3M_ARG((g.epilogue != K3M_EPI_BIAS_GELU && g.epilogue != K3M_EPI_DGELU) || g.aux);
+  K3M_ARG(g.f32_algo == K3M_F32_SPLIT_BF16X6 || g.f32_algo == K3M_F32_MFMA_F32);
   if (g.dtype == K3M_BF16) return k3m_gemm_bf16_impl(g, st);
   // A: K-contiguous iff a_trans == 0; B: K-contiguous iff b_trans == 1
   const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
@@ -95,7 +130,11 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
   // tile choice: the largest tile that still fills the 256 CUs; small co-attention GEMMs
   // (2,304-8,192 rows) otherwise leave CUs idle
   int rc;
-  if (vec && g.splitk <= 1 && (ak || bk) && nblocks(g, 256, 256) >= 200) rc = launch_tile_vec<256, 256, 2, 4, 1>(g, ak, bk, st);
+  if (vec && g.f32_algo == K3M_F32_SPLIT_BF16X6) {
+    if (g.splitk <= 1 && (ak || bk) && nblocks(g, 256, 256) >= 200) rc = launch_x6<256, 256, 2, 4, 16, 1>(g, ak, bk, st);
+    else if (g.splitk > 1 || nblocks(g, 128, 128) >= 256) rc = launch_x6<128, 128, 2, 2, 32, 1>(g, ak, bk, st);
+    else rc = launch_x6<64, 64, 2, 2, 32, 2>(g, ak, bk, st);
+  } else if (vec && g.splitk <= 1 && (ak || bk) && nblocks(g, 256, 256) >= 200) rc = launch_tile_vec<256, 256, 2, 4, 1>(g, ak, bk, st);
   else if (g.splitk > 1 || nblocks(g, 128, 128) >= 384) rc = launch_tile<128, 128, 2, 2, 2>(g, ak, bk, vec, st);
   else if (nblocks(g, 64, 128) >= 384) rc = launch_tile<64, 128, 2, 2, 2>(g, ak, bk, vec, st);
   else rc = launch_tile<64, 64, 2, 2, 2>(g, ak, bk, vec, st);

@@ -202,12 +202,12 @@ namespace k3m_f32 {
 // acc[i][j][r] holds row (r&3) + 8*(r>>2) + 4*(lane>>5), col lane&31 of MFMA tile (i, j).
 // Split-K (splitk > 1): the block's slab ws[blockIdx.y] gets the raw sum (alpha/beta are applied
 // by the reduction kernel).
-template <int TBM, int TBN, int WM, int WN, int EPI>
+template <int TBM, int TBN, int WM, int WN, int EPI, int CAP = 2 * (TBM + TBN) * BK>
 __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, float* smem,
                                          const floatx16 (&acc)[TBM / WM / 32][TBN / WN / 32]) {
   constexpr int FM = TBM / WM / 32, FN = TBN / WN / 32;
   constexpr int WCOLS = FN * 32, WS = WCOLS + 8, LPR = WCOLS / 8, RPP = 64 / LPR;
-  static_assert(WM * WN * 32 * WS <= 2 * (TBM + TBN) * BK, "epilogue staging exceeds the LDS tile");
+  static_assert(WM * WN * 32 * WS <= CAP, "epilogue staging exceeds the LDS tile");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = (w / WN) * (TBM / WM), wn = (w % WN) * (TBN / WN);
   const int kl = lane >> 5, cl = lane & 31;

@@ -1,5 +1,7 @@
 """Tensor-level wrappers over the C ABI (k3m_amd/_lib.py).  Every function launches libk3m_hip
 kernels on torch's current stream; torch is used only to allocate outputs/workspaces."""
+import os
+
 import torch
 
 from . import _lib as L
@@ -22,9 +24,15 @@ def empty(shape, like=None, dtype=torch.float32, device=None):
 
 
 # ------------------------------------------------------------------ GEMM
+# fp32-operand GEMM algorithm (include/k3m_hip.h K3mF32Algo): the bf16x6 split on the bf16 matrix
+# cores by default; K3M_F32_ALGO=mfma selects the exact-f32 v_mfma_f32_32x32x2_f32 kernels.
+F32_ALGO = {"x6": L.F32_SPLIT_BF16X6, "mfma": L.F32_MFMA_F32}[os.environ.get("K3M_F32_ALGO", "x6")]
+
+
 def gemm(a, a_trans, b, b_trans, c, m, n, k, epi=L.EPI_NONE, bias=None, aux=None, alpha=1.0, beta=0.0, splitk=1,
-         ws=None):
+         ws=None, f32_algo=None):
     g = L.K3mGemm()
+    g.f32_algo = F32_ALGO if f32_algo is None else f32_algo
     g.m, g.n, g.k = m, n, k
     g.a_trans, g.b_trans = a_trans, b_trans
     assert a.dtype == b.dtype, "A and B must share a dtype"

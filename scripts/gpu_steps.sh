@@ -19,6 +19,8 @@ step() {
 for s in "$@"; do
   case $s in
     kern) step kern 400 python -m pytest tests/test_gpu_kernels.py -q ;;
+    x6) step x6 400 python -m pytest tests/test_gpu_gemm_x6.py -q ;;
+    lab) step lab 300 scripts/lab/gemm_lab 10 ;;
     smoke) step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
     parity) step parity 900 python -m pytest tests/test_gpu_parity.py -x -q ;;
     gpu) step gputests 1200 python -m pytest tests -m gpu -q ;;

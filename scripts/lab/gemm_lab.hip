@@ -5,7 +5,7 @@
 #include <cmath>
 #include <vector>
 #include <string>
-#include "../../k3m_amd/csrc/gemm_f32_tile.h"
+#include "../../k3m_amd/csrc/gemm_x6_tile.h"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
@@ -43,15 +43,43 @@ void launch(const K3mGemm& g, hipStream_t st) {
   hipLaunchKernelGGL((gemm_f32_kernel<TBM, TBN, WM, WN, AK, BK_, true, EPI, OCC>), grid, dim3(64 * WM * WN), 0, st, g);
 }
 
+template <int TBM, int TBN, int WM, int WN, int BK, int OCC, int EPI, bool AK, bool BK_>
+void launch_x6(const K3mGemm& g, hipStream_t st) {
+  const int tm = (g.m + TBM - 1) / TBM, tn = (g.n + TBN - 1) / TBN;
+  dim3 grid(tm * tn, g.splitk > 1 ? g.splitk : 1);
+  hipLaunchKernelGGL((k3m_x6::gemm_x6_kernel<TBM, TBN, WM, WN, BK, AK, BK_, true, EPI, OCC>), grid, dim3(64 * WM * WN), 0, st, g);
+}
+
+// fp64 reference C = A.B^T (nt) for the accuracy check
+__global__ void ref64_kernel(const float* a, const float* b, int m, int n, int k, double* c) {
+  const int i = blockIdx.y, j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  double s = 0.0;
+  for (int l = 0; l < k; ++l) s += (double)a[(long long)i * k + l] * (double)b[(long long)j * k + l];
+  c[(long long)i * n + j] = s;
+}
+__global__ void err_kernel(const float* c, const double* r, long long n, double* out) {
+  double e2 = 0, emax = 0, rmax = 0;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const double d = (double)c[i] - r[i];
+    e2 += d * d; emax = fmax(emax, fabs(d)); rmax = fmax(rmax, fabs(r[i]));
+  }
+  atomicAdd(out, e2);
+  atomicMax((unsigned long long*)(out + 1), __double_as_longlong(emax));
+  atomicMax((unsigned long long*)(out + 2), __double_as_longlong(rmax));
+}
+
 struct Shape { const char* name; int kind; int m, n, k, epi, splitk; };  // kind 0 nt, 1 nn, 2 tn
 
 template <int EPI, bool AK, bool BK_>
 std::vector<std::pair<std::string, Launcher>> variants() {
   return {
-      {"v2 128x128 2x2 occ2", launch<128, 128, 2, 2, 2, EPI, AK, BK_>},
-      {"v2 256x128 4x2 occ1", launch<256, 128, 4, 2, 1, EPI, AK, BK_>},
-      {"v2 128x256 2x4 occ1", launch<128, 256, 2, 4, 1, EPI, AK, BK_>},
       {"v2 256x256 2x4 occ1", launch<256, 256, 2, 4, 1, EPI, AK, BK_>},
+      {"x6 256x256 2x4 bk16", launch_x6<256, 256, 2, 4, 16, 1, EPI, AK, BK_>},
+      {"x6 256x128 4x2 bk32", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_>},
+      {"x6 256x128 4x2 bk16", launch_x6<256, 128, 4, 2, 16, 1, EPI, AK, BK_>},
+      {"x6 128x128 2x2 bk16 o2", launch_x6<128, 128, 2, 2, 16, 2, EPI, AK, BK_>},
+      {"x6 128x128 2x2 bk32", launch_x6<128, 128, 2, 2, 32, 1, EPI, AK, BK_>},
   };
 }
 
@@ -96,6 +124,29 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill_kernel, dim3(64), dim3(256), 0, st, bias, 4096, 4ull, 0.5f);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  {
+    // accuracy vs fp64: C = A.B^T, m = n = 1024, k = 4096, A ~ U(-1,1), B ~ 0.05 U(-1,1)
+    const int m = 1024, n = 1024, k = 4096;
+    double *r64, *er;
+    CK(hipMalloc(&r64, (long long)m * n * 8)); CK(hipMalloc(&er, 24));
+    hipLaunchKernelGGL(ref64_kernel, dim3(n / 256, m), dim3(256), 0, st, a, b, m, n, k, r64);
+    K3mGemm g = {};
+    g.m = m; g.n = n; g.k = k; g.a_trans = 0; g.b_trans = 1; g.epilogue = 0; g.dtype = K3M_F32; g.c_dtype = K3M_F32;
+    g.splitk = 1; g.lda = k; g.ldb = k; g.ldc = n; g.a = a; g.b = b; g.c = c; g.alpha = 1.f; g.beta = 0.f;
+    auto report = [&](const char* name) {
+      CK(hipMemsetAsync(er, 0, 24, st));
+      hipLaunchKernelGGL(err_kernel, dim3(256), dim3(256), 0, st, c, r64, (long long)m * n, er);
+      double h[3];
+      CK(hipMemcpy(h, er, 24, hipMemcpyDeviceToHost));
+      printf("accuracy vs fp64 (1024x1024x4096 nt)  %-24s rms err %.3e  max err %.3e  max|ref| %.3e\n", name,
+             sqrt(h[0] / ((double)m * n)), h[1], h[2]);
+    };
+    k3m_gemm(&g, st); report("shipped f32 MFMA");
+    launch<256, 256, 2, 4, 1, 0, true, true>(g, st); report("v2 f32 MFMA 256x256");
+    launch_x6<256, 128, 4, 2, 32, 1, 0, true, true>(g, st); report("x6 bf16x6 256x128");
+    launch_x6<128, 128, 2, 2, 16, 2, 0, true, true>(g, st); report("x6 bf16x6 128x128");
+    fflush(stdout);
+  }
   for (const Shape& s : shapes) {
     K3mGemm g = {};
     g.m = s.m; g.n = s.n; g.k = s.k;
