@@ -2,9 +2,10 @@
 //
 // fp32 operands, default (K3M_F32_SPLIT_BF16X6): the bf16x6 split kernel of gemm_x6_tile.h on the
 // bf16 matrix cores (fp32 accuracy, 2.67x the f32-MFMA roofline), tile chosen per shape:
-//   * 256x256x16 (8 waves, 1 block/CU) for the large forward / input-gradient GEMMs;
-//   * 128x128x32 (4 waves) for split-K weight gradients and mid-size grids;
-//   * 64x64x32 for the small co-attention GEMMs.
+//   * 256x128x32 (8 waves, 1 block/CU, 144 KB LDS) for the large GEMMs and the split-K weight
+//     gradients (ops._splitk sizes the split to whole waves of 256 blocks);
+//   * 128x128x32 (4 waves) for mid-size grids;
+//   * 64x64x16 for the small co-attention GEMMs.
 // K3M_F32_MFMA_F32 (and unaligned operands): the v_mfma_f32_32x32x2_f32 kernel of gemm_f32_tile.h
 // (exact f32 products and accumulation), tile chosen per shape:
 //   * 256x256 (8 waves, 1 block/CU) when it still gives ~a block per CU: the fewest L2 bytes per FLOP;
@@ -131,9 +132,12 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
   // (2,304-8,192 rows) otherwise leave CUs idle
   int rc;
   if (vec && g.f32_algo == K3M_F32_SPLIT_BF16X6) {
-    if (g.splitk <= 1 && (ak || bk) && nblocks(g, 256, 256) >= 200) rc = launch_x6<256, 256, 2, 4, 16, 1>(g, ak, bk, st);
-    else if (g.splitk > 1 || nblocks(g, 128, 128) >= 256) rc = launch_x6<128, 128, 2, 2, 32, 1>(g, ak, bk, st);
-    else rc = launch_x6<64, 64, 2, 2, 32, 2>(g, ak, bk, st);
+    if (g.splitk > 1 || nblocks(g, 256, 128) >= 200) rc = launch_x6<256, 128, 4, 2, 32, 1>(g, ak, bk, st);
+    else if (nblocks(g, 128, 128) >= 200) rc = launch_x6<128, 128, 2, 2, 32, 1>(g, ak, bk, st);
+    // 64x64 runs at BK = 16: the BK = 32 build of this tile (ROCm 7.2 hipcc) returned C = alpha*AB
+    // without the beta*C term for scattered 16-lane groups (scripts/lab/gemm_dbg.hip reproduces it;
+    // tests/test_gpu_gemm_x6.py::test_x6_beta_all_tiles guards every tile path)
+    else rc = launch_x6<64, 64, 2, 2, 16, 2>(g, ak, bk, st);
   } else if (vec && g.splitk <= 1 && (ak || bk) && nblocks(g, 256, 256) >= 200) rc = launch_tile_vec<256, 256, 2, 4, 1>(g, ak, bk, st);
   else if (g.splitk > 1 || nblocks(g, 128, 128) >= 384) rc = launch_tile<128, 128, 2, 2, 2>(g, ak, bk, vec, st);
   else if (nblocks(g, 64, 128) >= 384) rc = launch_tile<64, 128, 2, 2, 2>(g, ak, bk, vec, st);

@@ -57,47 +57,76 @@ struct Stage {
   floatx4 r[NR];
 };
 
-template <bool KC, bool VEC, int TILE, int BK, int NT>
-__device__ __forceinline__ void load_tile(const float* __restrict__ p, long long ld, int mn0, int k0, int MN, int K,
-                                          Stage<KC, TILE, BK, NT>& s) {
-  const int t = threadIdx.x;
-  constexpr int NV = Stage<KC, TILE, BK, NT>::NV;
-  if constexpr (KC) {
-    constexpr int QR = BK / 4;  // float4 per row
+// Per-thread global source pointers of one operand tile, computed once per block and advanced by
+// one k-tile per step.  Rows / column groups past the M or N edge are clamped to a valid address:
+// what they load only reaches C rows / columns the epilogue never stores, so the steady-state loads
+// carry no masks or branches.  Only a partial last k-tile (K % BK != 0) is masked (load_tail).
+template <bool KC, int TILE, int BK, int NT>
+struct Src {
+  static constexpr int NB = Stage<KC, TILE, BK, NT>::NB;
+  const float* p[NB];
+  int kq[NB];    // k offset of the thread's first element inside the k-tile
+
+  __device__ __forceinline__ void init(const float* __restrict__ base, long long ld, int mn0, int kbeg, int MN) {
+    const int t = threadIdx.x;
 #pragma unroll
-    for (int it = 0; it < Stage<KC, TILE, BK, NT>::NB; ++it) {
-      const int idx = t + NT * it;
-      if (NV % NT != 0 && idx >= NV) break;
-      const int row = idx / QR, q = idx % QR;
-      const int gm = mn0 + row, gk = k0 + 4 * q;
-      if constexpr (VEC) {
-        s.r[it] = (gm < MN && gk < K) ? *reinterpret_cast<const floatx4*>(p + (long long)gm * ld + gk)
-                                      : floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < NB; ++b) {
+      const int idx = t + NT * b;
+      if constexpr (KC) {
+        const int row = idx / (BK / 4), q = idx % (BK / 4);
+        kq[b] = 4 * q;
+        p[b] = base + (long long)min(mn0 + row, MN - 1) * ld + kbeg + 4 * q;
       } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) s.r[it][e] = (gm < MN && gk + e < K) ? p[(long long)gm * ld + gk + e] : 0.f;
+        const int qm = idx % (TILE / 4), g4 = idx / (TILE / 4);
+        kq[b] = 4 * g4;
+        p[b] = base + (long long)(kbeg + 4 * g4) * ld + max(0, min(mn0 + 4 * qm, MN - 4));
       }
     }
-  } else {
-    constexpr int Q = TILE / 4;
+  }
+  __device__ __forceinline__ void advance(long long ld);
+};
+
+template <bool KC, int TILE, int BK, int NT>
+__device__ __forceinline__ void Src<KC, TILE, BK, NT>::advance(long long ld) {
 #pragma unroll
-    for (int b = 0; b < Stage<KC, TILE, BK, NT>::NB; ++b) {
-      const int idx = t + NT * b;
-      if (NV % NT != 0 && idx >= NV) break;
-      const int qm = idx % Q, g4 = idx / Q;
-      const int gm = mn0 + 4 * qm;
+  for (int b = 0; b < NB; ++b) p[b] += KC ? BK : BK * ld;
+}
+
+// Load the next full k-tile and advance the source pointers by one k-tile (16-B vectors; K % 4 == 0).
+template <bool KC, int TILE, int BK, int NT>
+__device__ __forceinline__ void load_full(Src<KC, TILE, BK, NT>& src, long long ld, Stage<KC, TILE, BK, NT>& s,
+                                          bool adv = true) {
+  constexpr int NB = Stage<KC, TILE, BK, NT>::NB, NV = Stage<KC, TILE, BK, NT>::NV;
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int gk = k0 + 4 * g4 + kk;
-        if constexpr (VEC) {
-          s.r[4 * b + kk] = (gk < K && gm < MN) ? *reinterpret_cast<const floatx4*>(p + (long long)gk * ld + gm)
-                                                : floatx4{0.f, 0.f, 0.f, 0.f};
-        } else {
+  for (int b = 0; b < NB; ++b) {
+    if (NV % NT != 0 && (int)threadIdx.x + NT * b >= NV) break;
+    if constexpr (KC) {
+      s.r[b] = *reinterpret_cast<const floatx4*>(src.p[b]);
+      src.p[b] += adv ? BK : 0;
+    } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            s.r[4 * b + kk][e] = (gk < K && gm + e < MN) ? p[(long long)gk * ld + gm + e] : 0.f;
-        }
-      }
+      for (int kk = 0; kk < 4; ++kk) s.r[4 * b + kk] = *reinterpret_cast<const floatx4*>(src.p[b] + kk * ld);
+      src.p[b] += adv ? BK * ld : 0;
+    }
+  }
+}
+
+// The partial last k-tile (pointers already advanced to it): krem (< BK, multiple of 4) k values
+// remain; the rest load as zeros.
+template <bool KC, int TILE, int BK, int NT>
+__device__ __forceinline__ void load_tail(const Src<KC, TILE, BK, NT>& src, long long ld, int krem,
+                                          Stage<KC, TILE, BK, NT>& s) {
+  constexpr int NB = Stage<KC, TILE, BK, NT>::NB, NV = Stage<KC, TILE, BK, NT>::NV;
+  const floatx4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if (NV % NT != 0 && (int)threadIdx.x + NT * b >= NV) break;
+    if constexpr (KC) {
+      s.r[b] = src.kq[b] < krem ? *reinterpret_cast<const floatx4*>(src.p[b]) : z;
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+        s.r[4 * b + kk] = src.kq[b] + kk < krem ? *reinterpret_cast<const floatx4*>(src.p[b] + kk * ld) : z;
     }
   }
 }
@@ -161,23 +190,15 @@ __device__ __forceinline__ void mainloop(const float* __restrict__ A, long long 
 
   Stage<AK, TBM, BK, NT> ra;
   Stage<BK_, TBN, BK, NT> rb;
-  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  if (nk > 0) {
-    load_tile<AK, VEC, TBM, BK, NT>(A, lda, m0, kbeg, M, kend, ra);
-    load_tile<BK_, VEC, TBN, BK, NT>(B, ldb, n0, kbeg, N, kend, rb);
-    store_tile<AK, TBM, BK, NT>(smem, ra);
-    store_tile<BK_, TBN, BK, NT>(smem + 3 * PA, rb);
-  }
-  __syncthreads();
+  Src<AK, TBM, BK, NT> sa;
+  Src<BK_, TBN, BK, NT> sb;
+  sa.init(A, lda, m0, kbeg, M);
+  sb.init(B, ldb, n0, kbeg, N);
+  const int klen = kend - kbeg;
+  const int nkf = klen > 0 ? klen / BK : 0;            // full k-tiles
+  const int krem = klen > 0 ? klen - nkf * BK : 0;     // k values of a partial last tile
   const int h = lane >> 5, cl = lane & 31;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) {
-      const int k0 = kbeg + (kt + 1) * BK;
-      load_tile<AK, VEC, TBM, BK, NT>(A, lda, m0, k0, M, kend, ra);
-      load_tile<BK_, VEC, TBN, BK, NT>(B, ldb, n0, k0, N, kend, rb);
-    }
+  auto compute = [&](int cur) {
     const __bf16* as = smem + cur * BUF;
     const __bf16* bs = as + 3 * PA;
 #pragma unroll
@@ -205,10 +226,54 @@ __device__ __forceinline__ void mainloop(const float* __restrict__ A, long long 
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
         }
     }
-    if (more) {
-      store_tile<AK, TBM, BK, NT>(smem + (cur ^ 1) * BUF, ra);
-      store_tile<BK_, TBN, BK, NT>(smem + (cur ^ 1) * BUF + 3 * PA, rb);
+  };
+  // Software pipeline, two register sets (unrolled by 2): during k-tile kt the LDS stage kt&1 is
+  // consumed by the MFMAs while the registers of tile kt+1 (loaded one iteration earlier, so their
+  // global latency is covered by a whole iteration) are split and written to the other stage in
+  // the same basic block, where the scheduler interleaves that VALU work with the MFMAs; tile
+  // kt+2 is loaded into the register set tile kt vacated.  Past the last full tile the loads
+  // re-read that tile (pointers stop advancing) and the spare stores hit an unread stage, so the
+  // steady state has no branches.
+  Stage<AK, TBM, BK, NT> ra1;
+  Stage<BK_, TBN, BK, NT> rb1;
+  if (nkf > 0) {
+    load_full<AK, TBM, BK, NT>(sa, lda, ra, nkf > 1);
+    load_full<BK_, TBN, BK, NT>(sb, ldb, rb, nkf > 1);
+    load_full<AK, TBM, BK, NT>(sa, lda, ra1, nkf > 2);
+    load_full<BK_, TBN, BK, NT>(sb, ldb, rb1, nkf > 2);
+    store_tile<AK, TBM, BK, NT>(smem, ra);
+    store_tile<BK_, TBN, BK, NT>(smem + 3 * PA, rb);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nkf; kt += 2) {
+    // even step: compute stage 0 | split ra1/rb1 (tile kt+1) -> stage 1 | load tile kt+2 -> ra/rb
+    load_full<AK, TBM, BK, NT>(sa, lda, ra, kt + 3 < nkf);
+    load_full<BK_, TBN, BK, NT>(sb, ldb, rb, kt + 3 < nkf);
+    compute(0);
+    store_tile<AK, TBM, BK, NT>(smem + BUF, ra1);
+    store_tile<BK_, TBN, BK, NT>(smem + BUF + 3 * PA, rb1);
+    __syncthreads();
+    if (kt + 1 >= nkf) break;
+    // odd step: compute stage 1 | split ra/rb (tile kt+2) -> stage 0 | load tile kt+3 -> ra1/rb1
+    load_full<AK, TBM, BK, NT>(sa, lda, ra1, kt + 4 < nkf);
+    load_full<BK_, TBN, BK, NT>(sb, ldb, rb1, kt + 4 < nkf);
+    compute(1);
+    store_tile<AK, TBM, BK, NT>(smem, ra);
+    store_tile<BK_, TBN, BK, NT>(smem + 3 * PA, rb);
+    __syncthreads();
+  }
+  if (krem > 0) {  // peeled partial k-tile (masked loads); the pointers rest on the last full tile
+    const int cur = nkf & 1;
+    if (nkf > 0) {
+      sa.advance(lda);
+      sb.advance(ldb);
     }
+    load_tail<AK, TBM, BK, NT>(sa, lda, krem, ra);
+    load_tail<BK_, TBN, BK, NT>(sb, ldb, krem, rb);
+    store_tile<AK, TBM, BK, NT>(smem + cur * BUF, ra);
+    store_tile<BK_, TBN, BK, NT>(smem + cur * BUF + 3 * PA, rb);
+    __syncthreads();
+    compute(cur);
     __syncthreads();
   }
 }

@@ -68,7 +68,21 @@ def linear_dgrad(dy, W, dx=None, beta=0.0, dgelu_aux=None, alpha=1.0):
     return gemm(dy, 0, W, 0, dx, M, K, N, epi, None, dgelu_aux, alpha, beta)
 
 
-def _splitk(m, n, k):
+def _splitk(m, n, k, dtype=torch.float32):
+    """K-split of a weight-gradient GEMM (C[m,n] summed over k ~ 20k rows): enough blocks to fill
+    the 256 CUs in whole waves.  fp32 (bf16x6 kernel) tiles are 256x128 at one block per CU;
+    bf16 tiles are 128x128 at two per CU."""
+    if dtype == torch.float32 and F32_ALGO == L.F32_SPLIT_BF16X6:
+        tiles = ((m + 255) // 256) * ((n + 127) // 128)
+        if tiles >= 200 or k < 2048:
+            return 1
+        # minimise (waves of 256 blocks) x (k per split), plus ~1% per split for the slab reduction
+        best, best_cost = 1, float("inf")
+        for s in range(1, min(32, k // 1024) + 1):
+            cost = ((tiles * s + 255) // 256) / s * (1.0 + 0.01 * s)
+            if cost < best_cost - 1e-9:
+                best, best_cost = s, cost
+        return best
     tiles = ((m + 127) // 128) * ((n + 127) // 128)
     if tiles >= 384 or k < 1024:
         return 1
@@ -81,7 +95,7 @@ def linear_wgrad(dy, x, gW, gb=None, alpha=1.0):
     dy's producer).  dy [M,N], x [M,K], gW [N,K] fp32."""
     M, N = dy.shape
     K = x.shape[1]
-    s = _splitk(N, K, M)
+    s = _splitk(N, K, M, dy.dtype)
     ws = torch.empty((s * N * K,), dtype=torch.float32, device=dy.device) if s > 1 else None
     gemm(dy, 1, x, 0, gW, N, K, M, L.EPI_NONE, None, None, alpha, 1.0, s, ws)
     if gb is not None:

@@ -77,7 +77,6 @@ std::vector<std::pair<std::string, Launcher>> variants() {
       {"v2 256x256 2x4 occ1", launch<256, 256, 2, 4, 1, EPI, AK, BK_>},
       {"x6 256x256 2x4 bk16", launch_x6<256, 256, 2, 4, 16, 1, EPI, AK, BK_>},
       {"x6 256x128 4x2 bk32", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_>},
-      {"x6 256x128 4x2 bk16", launch_x6<256, 128, 4, 2, 16, 1, EPI, AK, BK_>},
       {"x6 128x128 2x2 bk16 o2", launch_x6<128, 128, 2, 2, 16, 2, EPI, AK, BK_>},
       {"x6 128x128 2x2 bk32", launch_x6<128, 128, 2, 2, 32, 1, EPI, AK, BK_>},
   };
@@ -108,6 +107,10 @@ int main(int argc, char** argv) {
       {"wgrad ffn1 s5", 2, 3072, 768, M, 0, 5},
       {"wgrad ffn2 s5", 2, 768, 3072, M, 0, 5},
       {"wgrad qkv s2", 2, 2304, 768, M, 0, 2},
+      {"wgrad ffn1 s7", 2, 3072, 768, M, 0, 7},
+      {"wgrad qkv s9", 2, 2304, 768, M, 0, 9},
+      {"wgrad out s28", 2, 768, 768, M, 0, 28},
+      {"wgrad out s8", 2, 768, 768, M, 0, 8},
       {"co pv ffn1 gelu", 0, 8192, 3072, 768, 2, 1},
       {"co txt ffn2", 0, 2304, 768, 3072, 1, 1},
   };

@@ -77,3 +77,24 @@ def test_x6_epilogues_match_torch(dev):
     xr = aux.clone().requires_grad_(True)
     torch.nn.functional.gelu(xr).backward((dy.double() @ W.double()).float())
     assert float((dx - xr.grad).abs().max()) < 2e-5 * float(xr.grad.abs().max())
+
+
+@pytest.mark.parametrize("m,n,k", [(4096, 3072, 768), (2304, 2304, 768), (1000, 3072, 768), (1024, 1024, 2048)])
+@pytest.mark.parametrize("at,bt", [(0, 1), (0, 0), (1, 0)])
+def test_x6_beta_all_tiles(dev, m, n, k, at, bt):
+    """C = alpha*op(A)op(B) + beta*C on every x6 tile path (256x128, 128x128, 64x64), repeated: the
+    read-modify-write of C must see the old value in every lane (regression for a 64x64 BK=32 build)."""
+    from k3m_amd import ops, _lib as L
+    g = torch.Generator(device="cpu").manual_seed(m * 7 + n + k)
+    A = torch.randn(m, k, generator=g)
+    Bm = torch.randn(k, n, generator=g)
+    C0 = torch.randn(m, n, generator=g)
+    ref = 0.5 * (A.double() @ Bm.double()) + 0.25 * C0.double()
+    a = (A.t().contiguous() if at else A).to(dev)
+    b = (Bm.t().contiguous() if bt else Bm).to(dev)
+    c0 = C0.to(dev)
+    for _ in range(5):
+        c = c0.clone()
+        ops.gemm(a, at, b, bt, c, m, n, k, alpha=0.5, beta=0.25, f32_algo=L.F32_SPLIT_BF16X6)
+        err = float((c.double().cpu() - ref).abs().max())
+        assert err < 2e-5 * float(ref.abs().max()), err
