@@ -24,7 +24,6 @@
 namespace k3m_x6 {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));
 
 template <int BK>
@@ -34,18 +33,32 @@ __device__ __forceinline__ int slot_off(int r, int c) {
   return r * BK + ((c ^ ((r >> SH) & (CPR - 1))) << 3);
 }
 
-// exact three-way split of 4 floats into bf16 planes (round-to-nearest-even at each level)
-__device__ __forceinline__ void split4(const floatx4 v, bf16x4& h, bf16x4& m, bf16x4& l) {
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const __bf16 hb = (__bf16)v[e];
-    const float r1 = v[e] - (float)hb;
-    const __bf16 mb = (__bf16)r1;
-    const float r2 = r1 - (float)mb;
-    h[e] = hb;
-    m[e] = mb;
-    l[e] = (__bf16)r2;
-  }
+typedef float float2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+
+// two floats -> packed bf16 pair, round-to-nearest-even (one v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((float2v{a, b}), bf16x2v));
+}
+
+// exact three-way split of a float pair into packed bf16 planes h, m, l (a = h + m + l exactly):
+// per pair 3 conversions, 2 x (unpack lo/hi + subtract) = ~4.5 VALU per element
+__device__ __forceinline__ void split2(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = pk_bf16(a, b);
+  const float r1a = a - __uint_as_float(h << 16), r1b = b - __uint_as_float(h & 0xffff0000u);
+  m = pk_bf16(r1a, r1b);
+  const float r2a = r1a - __uint_as_float(m << 16), r2b = r1b - __uint_as_float(m & 0xffff0000u);
+  l = pk_bf16(r2a, r2b);
+}
+
+__device__ __forceinline__ void split4(const floatx4 v, u32x2v& h, u32x2v& m, u32x2v& l) {
+  uint32_t h0, m0, l0, h1, m1, l1;
+  split2(v[0], v[1], h0, m0, l0);
+  split2(v[2], v[3], h1, m1, l1);
+  h = u32x2v{h0, h1};
+  m = u32x2v{m0, m1};
+  l = u32x2v{l0, l1};
 }
 
 template <bool KC, int TILE, int BK, int NT>
@@ -144,11 +157,11 @@ __device__ __forceinline__ void store_tile(__bf16* __restrict__ lds, const Stage
       if (NV % NT != 0 && idx >= NV) break;
       const int row = idx / QR, q = idx % QR;
       const int off = slot_off<BK>(row, q >> 1) + 4 * (q & 1);
-      bf16x4 h, m, l;
+      u32x2v h, m, l;
       split4(s.r[it], h, m, l);
-      *reinterpret_cast<bf16x4*>(lds + off) = h;
-      *reinterpret_cast<bf16x4*>(lds + PL + off) = m;
-      *reinterpret_cast<bf16x4*>(lds + 2 * PL + off) = l;
+      *reinterpret_cast<u32x2v*>(lds + off) = h;
+      *reinterpret_cast<u32x2v*>(lds + PL + off) = m;
+      *reinterpret_cast<u32x2v*>(lds + 2 * PL + off) = l;
     }
   } else {
     constexpr int Q = TILE / 4;
@@ -161,11 +174,11 @@ __device__ __forceinline__ void store_tile(__bf16* __restrict__ lds, const Stage
       for (int e = 0; e < 4; ++e) {
         const floatx4 v = {s.r[4 * b][e], s.r[4 * b + 1][e], s.r[4 * b + 2][e], s.r[4 * b + 3][e]};
         const int off = slot_off<BK>(4 * qm + e, g4 >> 1) + 4 * (g4 & 1);
-        bf16x4 h, m, l;
+        u32x2v h, m, l;
         split4(v, h, m, l);
-        *reinterpret_cast<bf16x4*>(lds + off) = h;
-        *reinterpret_cast<bf16x4*>(lds + PL + off) = m;
-        *reinterpret_cast<bf16x4*>(lds + 2 * PL + off) = l;
+        *reinterpret_cast<u32x2v*>(lds + off) = h;
+        *reinterpret_cast<u32x2v*>(lds + PL + off) = m;
+        *reinterpret_cast<u32x2v*>(lds + 2 * PL + off) = l;
       }
     }
   }

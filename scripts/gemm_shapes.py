@@ -9,7 +9,7 @@ for r in rows:
     name = r["Kernel_Name"]
     if "gemm" not in name and "attn" not in name:
         continue
-    key = (name.replace("void ", "").replace("(anonymous namespace)::", "").split("(K3m")[0].split("(float")[0][:60], int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]),
+    key = (name.replace("void ", "").replace("(anonymous namespace)::", "").replace("k3m_x6::", "").split("(K3m")[0].split("(float")[0][:60], int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]),
            int(r["Grid_Size_Y"]))
     agg[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 tot = sum(sum(v) for v in agg.values())

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <vector>
 #include <string>
+#include <cstring>
 #include "../../k3m_amd/csrc/gemm_x6_tile.h"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
@@ -94,6 +95,9 @@ std::vector<std::pair<std::string, Launcher>> variants_epi(int epi) {
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 10;
+  const char* only_shape = argc > 2 ? argv[2] : nullptr;    // substring filters (profiling runs)
+  const char* only_var = argc > 3 ? argv[3] : nullptr;
+  const bool skip_acc = only_shape != nullptr;
   const int M = 20992;
   std::vector<Shape> shapes = {
       {"sq4096 nt", 0, 4096, 4096, 4096, 0, 1},
@@ -127,7 +131,7 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill_kernel, dim3(64), dim3(256), 0, st, bias, 4096, 4ull, 0.5f);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  {
+  if (!skip_acc) {
     // accuracy vs fp64: C = A.B^T, m = n = 1024, k = 4096, A ~ U(-1,1), B ~ 0.05 U(-1,1)
     const int m = 1024, n = 1024, k = 4096;
     double *r64, *er;
@@ -151,6 +155,7 @@ int main(int argc, char** argv) {
     fflush(stdout);
   }
   for (const Shape& s : shapes) {
+    if (only_shape && !strstr(s.name, only_shape)) continue;
     K3mGemm g = {};
     g.m = s.m; g.n = s.n; g.k = s.k;
     g.a_trans = s.kind == 2; g.b_trans = s.kind == 0;
@@ -180,6 +185,7 @@ int main(int argc, char** argv) {
     std::vector<std::pair<std::string, Launcher>> vs =
         s.kind == 0 ? variants_epi<true, true>(s.epi) : s.kind == 1 ? variants_epi<true, false>(s.epi) : variants_epi<false, false>(s.epi);
     for (auto& v : vs) {
+      if (only_var && !strstr(v.first.c_str(), only_var)) continue;
       K3mGemm gv = g;
       gv.c = c;
       auto go = [&]() {
