@@ -40,7 +40,7 @@ def parse():
                     help="fp32: configs[1] (the metric's config); bf16: mixed-precision encoder (configs[2])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=2)
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=10)
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL) for real runs; gloo only to rehearse the "
                     "multi-rank path with several ranks sharing one GPU")
     return ap.parse_args()

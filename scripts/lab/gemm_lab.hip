@@ -75,11 +75,10 @@ struct Shape { const char* name; int kind; int m, n, k, epi, splitk; };  // kind
 template <int EPI, bool AK, bool BK_>
 std::vector<std::pair<std::string, Launcher>> variants() {
   return {
-      {"v2 256x256 2x4 occ1", launch<256, 256, 2, 4, 1, EPI, AK, BK_>},
       {"x6 256x256 2x4 bk16", launch_x6<256, 256, 2, 4, 16, 1, EPI, AK, BK_>},
       {"x6 256x128 4x2 bk32", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_>},
-      {"x6 128x128 2x2 bk16 o2", launch_x6<128, 128, 2, 2, 16, 2, EPI, AK, BK_>},
       {"x6 128x128 2x2 bk32", launch_x6<128, 128, 2, 2, 32, 1, EPI, AK, BK_>},
+      {"x6 64x64 2x2 bk16 o2", launch_x6<64, 64, 2, 2, 16, 2, EPI, AK, BK_>},
   };
 }
 
