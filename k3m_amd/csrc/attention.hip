@@ -21,8 +21,11 @@ namespace {
 
 constexpr int MAXL = 128;
 constexpr int MAXD = 128;
-constexpr int NW = 8;          // waves per workgroup
-constexpr int NTH = NW * 64;
+// Two builds of each kernel: (ML = 128, 8 waves) for any sequence up to 128, and (ML = 64, 4 waves)
+// for sequences up to 64 (the text, image and text<->image co-attention cases: L = 36/37).  The
+// short build's register arrays are sized for 64 rows, so it holds ~half the VGPRs and, with its
+// <= 80 KB of LDS, two or three workgroups share a CU — the L <= 64 cases are latency-bound, and
+// one 8-wave workgroup per CU left most of each block's global-load and barrier waits exposed.
 
 __device__ __forceinline__ int sw(int i, int c, int cols) { return i * cols + (c ^ (i & 31)); }
 
@@ -30,20 +33,20 @@ __device__ __forceinline__ int sw(int i, int c, int cols) { return i * cols + (c
 // current phase's MFMAs and written after its barrier: every thread loads its 16-byte chunks
 // (8 bf16 / 4 fp32 of one row) into registers first — one HBM latency per operand, not one per
 // element — then converts and writes them into the swizzled fp32 image (rows >= nvalid are zero).
-template <typename T>
+template <typename T, int ML, int NTH>
 struct Chunks {
   static constexpr int VE = 16 / sizeof(T);
-  static constexpr int N = MAXL * MAXD / VE / NTH;  // chunks per thread for the largest tile
+  static constexpr int N = ML * MAXD / VE / NTH;  // chunks per thread for the largest tile
   uint4 r[N];
 };
 
-template <typename T>
-__device__ __forceinline__ void stage_load(Chunks<T>& ch, const T* __restrict__ src, long long row0, long long ld,
+template <typename T, int ML, int NTH>
+__device__ __forceinline__ void stage_load(Chunks<T, ML, NTH>& ch, const T* __restrict__ src, long long row0, long long ld,
                                            int coff, int nrows, int nvalid, int cols) {
-  constexpr int VE = Chunks<T>::VE;
+  constexpr int VE = Chunks<T, ML, NTH>::VE;
   const int cpr = cols / VE, nch = nrows * cpr;
 #pragma unroll
-  for (int u = 0; u < Chunks<T>::N; ++u) {
+  for (int u = 0; u < Chunks<T, ML, NTH>::N; ++u) {
     const int e = threadIdx.x + u * NTH;
     ch.r[u] = make_uint4(0u, 0u, 0u, 0u);
     if (e < nch) {
@@ -53,12 +56,12 @@ __device__ __forceinline__ void stage_load(Chunks<T>& ch, const T* __restrict__ 
   }
 }
 
-template <typename T>
-__device__ __forceinline__ void stage_store(float* __restrict__ dst, const Chunks<T>& ch, int nrows, int cols) {
-  constexpr int VE = Chunks<T>::VE;
+template <typename T, int ML, int NTH>
+__device__ __forceinline__ void stage_store(float* __restrict__ dst, const Chunks<T, ML, NTH>& ch, int nrows, int cols) {
+  constexpr int VE = Chunks<T, ML, NTH>::VE;
   const int cpr = cols / VE, nch = nrows * cpr;
 #pragma unroll
-  for (int u = 0; u < Chunks<T>::N; ++u) {
+  for (int u = 0; u < Chunks<T, ML, NTH>::N; ++u) {
     const int e = threadIdx.x + u * NTH;
     if (e < nch) {
       const int i = e / cpr, c = (e - i * cpr) * VE;
@@ -77,22 +80,23 @@ __device__ __forceinline__ void stage_store(float* __restrict__ dst, const Chunk
   }
 }
 
-template <typename T>
+template <typename T, int ML, int NTH>
 __device__ __forceinline__ void stage(float* __restrict__ dst, const T* __restrict__ src, long long row0, long long ld,
                                       int coff, int nrows, int nvalid, int cols) {
-  Chunks<T> ch;
+  Chunks<T, ML, NTH> ch;
   stage_load(ch, src, row0, ld, coff, nrows, nvalid, cols);
   stage_store(dst, ch, nrows, cols);
 }
 
 // ------------------------------------------------------------------ forward
-template <typename T>
-__global__ __launch_bounds__(NTH) void attn_fwd_kernel(const T* __restrict__ q, long long ldq, const T* __restrict__ k,
+template <typename T, int ML, int NW>
+__global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_fwd_kernel(const T* __restrict__ q, long long ldq, const T* __restrict__ k,
                                                        long long ldk, const T* __restrict__ v, long long ldv,
                                                        const float* __restrict__ kmask, T* __restrict__ ctx,
                                                        long long ldc, float* __restrict__ probs, int lq, int lk,
                                                        int nh, int hd, float scale, float p_drop, uint64_t seed,
                                                        uint64_t off) {
+  constexpr int NTH = NW * 64;
   extern __shared__ float smem[];
   const int s = blockIdx.x / nh, h = blockIdx.x % nh;
   const int LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
@@ -104,10 +108,10 @@ __global__ __launch_bounds__(NTH) void attn_fwd_kernel(const T* __restrict__ q, 
   const int hoff = h * hd;
   const long long pbase = ((long long)s * nh + h) * lq * lk;
 
-  stage(Qs, q, qrow0, ldq, hoff, LQ, lq, hd);
-  stage(KVs, k, krow0, ldk, hoff, LK, lk, hd);
+  stage<T, ML, NTH>(Qs, q, qrow0, ldq, hoff, LQ, lq, hd);
+  stage<T, ML, NTH>(KVs, k, krow0, ldk, hoff, LK, lk, hd);
   __syncthreads();
-  Chunks<T> vch;  // V's loads fly while S is computed
+  Chunks<T, ML, NTH> vch;  // V's loads fly while S is computed
   stage_load(vch, v, krow0, ldv, hoff, LK, lk, hd);
   // S = scale * Q K^T + mask
   {
@@ -191,8 +195,8 @@ __global__ __launch_bounds__(NTH) void attn_fwd_kernel(const T* __restrict__ q, 
 //   dQ   = scale * dS K                     phase 2  (R2 <- K)
 //   dV   = Pd^T dO                          phase 3  (R2 <- Pd)
 //   dK   = scale * dS^T Q                   phase 4  (R1 <- Q)
-template <typename T>
-__global__ __launch_bounds__(NTH) void attn_bwd_kernel(const T* __restrict__ dctx, long long ldc,
+template <typename T, int ML, int NW>
+__global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(const T* __restrict__ dctx, long long ldc,
                                                        const T* __restrict__ o, long long ldo,
                                                        const T* __restrict__ q, long long ldq, const T* __restrict__ k,
                                                        long long ldk, const T* __restrict__ v, long long ldv,
@@ -200,6 +204,7 @@ __global__ __launch_bounds__(NTH) void attn_bwd_kernel(const T* __restrict__ dct
                                                        T* __restrict__ dk, T* __restrict__ dv, long long lddq,
                                                        long long lddk, long long lddv, int lq, int lk, int nh, int hd,
                                                        float scale, float p_drop, uint64_t seed, uint64_t off) {
+  constexpr int NTH = NW * 64;
   extern __shared__ float smem[];
   const int s = blockIdx.x / nh, h = blockIdx.x % nh;
   const int LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
@@ -215,11 +220,11 @@ __global__ __launch_bounds__(NTH) void attn_bwd_kernel(const T* __restrict__ dct
   const int hoff = h * hd;
   const long long pbase = ((long long)s * nh + h) * lq * lk;
 
-  stage(R1, dctx, qrow0, ldc, hoff, LQ, lq, hd);
-  stage(R2, v, krow0, ldv, hoff, LK, lk, hd);
+  stage<T, ML, NTH>(R1, dctx, qrow0, ldc, hoff, LQ, lq, hd);
+  stage<T, ML, NTH>(R2, v, krow0, ldv, hoff, LK, lk, hd);
   // D_i = dO_i . O_i: a wave per row, lanes over the head dimension (all loads issued first)
   {
-    constexpr int RW = MAXL / NW;   // rows per wave
+    constexpr int RW = ML / NW;     // rows per wave
     float pa[RW][MAXD / 64], pb[RW][MAXD / 64];
 #pragma unroll
     for (int u = 0; u < RW; ++u) {
@@ -243,7 +248,7 @@ __global__ __launch_bounds__(NTH) void attn_bwd_kernel(const T* __restrict__ dct
     }
   }
   __syncthreads();
-  Chunks<T> nch;  // K's loads fly during phase 1
+  Chunks<T, ML, NTH> nch;  // K's loads fly during phase 1
   stage_load(nch, k, krow0, ldk, hoff, LK, lk, hd);
   // phase 1: dS
   {
@@ -298,7 +303,7 @@ __global__ __launch_bounds__(NTH) void attn_bwd_kernel(const T* __restrict__ dct
   __syncthreads();
   // phase 3: R2 <- Pd [LQ][LK]; dV = Pd^T dO
   {
-    constexpr int U = MAXL * MAXL / NTH;
+    constexpr int U = ML * ML / NTH;
     float pv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {   // all loads first
@@ -378,14 +383,35 @@ bool vec_ok(const void* p, long long ld, int dtype) {
   return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % ve == 0;
 }
 
-template <typename T>
+template <typename T, int ML, int NW>
 void set_lds_attr() {
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<T, ML, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<T, ML, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     done = true;
   }
+}
+
+template <typename T, int ML, int NW>
+void launch_fwd(const void* q, long long ldq, const void* k, long long ldk, const void* v, long long ldv,
+                const float* kmask, void* ctx, long long ldc, float* probs, int nseq, int lq, int lk, int nh, int hd,
+                float scale, float p_drop, uint64_t seed, uint64_t off, size_t lds, hipStream_t st) {
+  set_lds_attr<T, ML, NW>();
+  hipLaunchKernelGGL((attn_fwd_kernel<T, ML, NW>), dim3(nseq * nh), dim3(NW * 64), lds, st, (const T*)q, ldq,
+                     (const T*)k, ldk, (const T*)v, ldv, kmask, (T*)ctx, ldc, probs, lq, lk, nh, hd, scale, p_drop,
+                     seed, off);
+}
+
+template <typename T, int ML, int NW>
+void launch_bwd(const void* dctx, long long ldc, const void* o, long long ldo, const void* q, long long ldq,
+                const void* k, long long ldk, const void* v, long long ldv, const float* probs, void* dq, void* dk,
+                void* dv, long long lddq, long long lddk, long long lddv, int nseq, int lq, int lk, int nh, int hd,
+                float scale, float p_drop, uint64_t seed, uint64_t off, size_t lds, hipStream_t st) {
+  set_lds_attr<T, ML, NW>();
+  hipLaunchKernelGGL((attn_bwd_kernel<T, ML, NW>), dim3(nseq * nh), dim3(NW * 64), lds, st, (const T*)dctx, ldc,
+                     (const T*)o, ldo, (const T*)q, ldq, (const T*)k, ldk, (const T*)v, ldv, probs, (T*)dq, (T*)dk,
+                     (T*)dv, lddq, lddk, lddv, lq, lk, nh, hd, scale, p_drop, seed, off);
 }
 
 }  // namespace
@@ -398,20 +424,16 @@ extern "C" int k3m_attn_fwd(const void* q, long long ldq, const void* k, long lo
   K3M_ARG(lq > 0 && lq <= MAXL && lk > 0 && lk <= MAXL && hd > 0 && hd <= MAXD && hd % 32 == 0 && nh > 0);
   if (nseq == 0) return 0;
   K3M_ARG(vec_ok(q, ldq, dtype) && vec_ok(k, ldk, dtype) && vec_ok(v, ldv, dtype));
+  K3M_ARG(dtype == K3M_F32 || dtype == K3M_BF16);
   const size_t lds = fwd_lds(lq, lk, hd);
   K3M_ARG(lds <= (size_t)LDS_MAX);
+  const bool small = false;   // the forward gains nothing from the short build (measured)
   if (dtype == K3M_F32) {
-    set_lds_attr<float>();
-    hipLaunchKernelGGL(attn_fwd_kernel<float>, dim3(nseq * nh), dim3(NTH), lds, st, (const float*)q, ldq,
-                       (const float*)k, ldk, (const float*)v, ldv, kmask, (float*)ctx, ldc, probs, lq, lk, nh, hd,
-                       scale, p_drop, seed, off);
-  } else if (dtype == K3M_BF16) {
-    set_lds_attr<bf16_t>();
-    hipLaunchKernelGGL(attn_fwd_kernel<bf16_t>, dim3(nseq * nh), dim3(NTH), lds, st, (const bf16_t*)q, ldq,
-                       (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, kmask, (bf16_t*)ctx, ldc, probs, lq, lk, nh, hd,
-                       scale, p_drop, seed, off);
+    if (small) launch_fwd<float, 64, 4>(q, ldq, k, ldk, v, ldv, kmask, ctx, ldc, probs, nseq, lq, lk, nh, hd, scale, p_drop, seed, off, lds, st);
+    else launch_fwd<float, 128, 8>(q, ldq, k, ldk, v, ldv, kmask, ctx, ldc, probs, nseq, lq, lk, nh, hd, scale, p_drop, seed, off, lds, st);
   } else {
-    return K3M_EINVAL;
+    if (small) launch_fwd<bf16_t, 64, 4>(q, ldq, k, ldk, v, ldv, kmask, ctx, ldc, probs, nseq, lq, lk, nh, hd, scale, p_drop, seed, off, lds, st);
+    else launch_fwd<bf16_t, 128, 8>(q, ldq, k, ldk, v, ldv, kmask, ctx, ldc, probs, nseq, lq, lk, nh, hd, scale, p_drop, seed, off, lds, st);
   }
   K3M_CHECK_LAUNCH();
   return 0;
@@ -426,21 +448,16 @@ extern "C" int k3m_attn_bwd(const void* dctx, long long ldc, const void* o, long
   K3M_ARG(lq > 0 && lq <= MAXL && lk > 0 && lk <= MAXL && hd > 0 && hd <= MAXD && hd % 32 == 0 && nh > 0);
   if (nseq == 0) return 0;
   K3M_ARG(vec_ok(q, ldq, dtype) && vec_ok(k, ldk, dtype) && vec_ok(v, ldv, dtype) && vec_ok(dctx, ldc, dtype));
+  K3M_ARG(dtype == K3M_F32 || dtype == K3M_BF16);
   const size_t lds = bwd_lds(lq, lk, hd);
   K3M_ARG(lds <= (size_t)LDS_MAX);
+  const bool small = lq <= 64 && lk <= 64 && hd <= 64;   // d = 128 runs better as one 8-wave block
   if (dtype == K3M_F32) {
-    set_lds_attr<float>();
-    hipLaunchKernelGGL(attn_bwd_kernel<float>, dim3(nseq * nh), dim3(NTH), lds, st, (const float*)dctx, ldc,
-                       (const float*)o, ldo, (const float*)q, ldq, (const float*)k, ldk, (const float*)v, ldv, probs,
-                       (float*)dq, (float*)dk, (float*)dv, lddq, lddk, lddv, lq, lk, nh, hd, scale, p_drop, seed, off);
-  } else if (dtype == K3M_BF16) {
-    set_lds_attr<bf16_t>();
-    hipLaunchKernelGGL(attn_bwd_kernel<bf16_t>, dim3(nseq * nh), dim3(NTH), lds, st, (const bf16_t*)dctx, ldc,
-                       (const bf16_t*)o, ldo, (const bf16_t*)q, ldq, (const bf16_t*)k, ldk, (const bf16_t*)v, ldv,
-                       probs, (bf16_t*)dq, (bf16_t*)dk, (bf16_t*)dv, lddq, lddk, lddv, lq, lk, nh, hd, scale, p_drop,
-                       seed, off);
+    if (small) launch_bwd<float, 64, 4>(dctx, ldc, o, ldo, q, ldq, k, ldk, v, ldv, probs, dq, dk, dv, lddq, lddk, lddv, nseq, lq, lk, nh, hd, scale, p_drop, seed, off, lds, st);
+    else launch_bwd<float, 128, 8>(dctx, ldc, o, ldo, q, ldq, k, ldk, v, ldv, probs, dq, dk, dv, lddq, lddk, lddv, nseq, lq, lk, nh, hd, scale, p_drop, seed, off, lds, st);
   } else {
-    return K3M_EINVAL;
+    if (small) launch_bwd<bf16_t, 64, 4>(dctx, ldc, o, ldo, q, ldq, k, ldk, v, ldv, probs, dq, dk, dv, lddq, lddk, lddv, nseq, lq, lk, nh, hd, scale, p_drop, seed, off, lds, st);
+    else launch_bwd<bf16_t, 128, 8>(dctx, ldc, o, ldo, q, ldq, k, ldk, v, ldv, probs, dq, dk, dv, lddq, lddk, lddv, nseq, lq, lk, nh, hd, scale, p_drop, seed, off, lds, st);
   }
   K3M_CHECK_LAUNCH();
   return 0;

@@ -42,6 +42,33 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((float2v{a, b}), bf16x2v));
 }
 
+// MN-contiguous operand image: a [BK k][TILE mn] bf16 plane (rows of TILE/8 16-B chunks), chunk ch of
+// row k at slot ch ^ swz(k).  The staging writes of 16 lanes are 128 contiguous bytes of one row
+// (conflict-free), and the transposing fragment reads (ds_read_b64_tr_b16: per 16-lane group 4 rows
+// x 16 columns) put the 4 rows x 4 chunks of a 32-lane half on 16 distinct bank quads.
+template <int TILE>
+__device__ __forceinline__ int mn_off(int k, int ch) {
+  if constexpr (TILE >= 128) return k * TILE + ((ch ^ (((k & 3) << 2) | ((k >> 2) & 3))) << 3);
+  else return k * TILE + ((ch ^ (((k >> 1) & 1) << 2)) << 3);
+}
+
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef short short8v __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) short4v lds_short4v;
+
+// MFMA operand fragment of an MN image: element e of lane l = X[16 ks + 8 (l>>5) + e][mn_base + (l&31)]
+// (the same k order as the k-contiguous fragments), from two transposing reads.
+template <int TILE>
+__device__ __forceinline__ bf16x8 mn_frag(const __bf16* img, int mn_base, int ks, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, h = lane >> 5;
+  const int ch = ((mn_base + 16 * (g & 1)) >> 3) + (p >> 1);
+  const int r0 = 16 * ks + 8 * h + q;
+  const short4v x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(img + mn_off<TILE>(r0, ch) + 4 * (p & 1)));
+  const short4v x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(img + mn_off<TILE>(r0 + 4, ch) + 4 * (p & 1)));
+  const short8v v = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 // exact three-way split of a float pair into packed bf16 planes h, m, l (a = h + m + l exactly):
 // per pair 3 conversions, 2 x (unpack lo/hi + subtract) = ~4.5 VALU per element
 __device__ __forceinline__ void split2(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
@@ -171,11 +198,10 @@ __device__ __forceinline__ void store_tile(__bf16* __restrict__ lds, const Stage
       if (NV % NT != 0 && idx >= NV) break;
       const int qm = idx % Q, g4 = idx / Q;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const floatx4 v = {s.r[4 * b][e], s.r[4 * b + 1][e], s.r[4 * b + 2][e], s.r[4 * b + 3][e]};
-        const int off = slot_off<BK>(4 * qm + e, g4 >> 1) + 4 * (g4 & 1);
+      for (int kk = 0; kk < 4; ++kk) {   // k row 4 g4 + kk, columns 4 qm .. 4 qm + 3
+        const int off = mn_off<TILE>(4 * g4 + kk, qm >> 1) + 4 * (qm & 1);
         u32x2v h, m, l;
-        split4(v, h, m, l);
+        split4(s.r[4 * b + kk], h, m, l);
         *reinterpret_cast<u32x2v*>(lds + off) = h;
         *reinterpret_cast<u32x2v*>(lds + PL + off) = m;
         *reinterpret_cast<u32x2v*>(lds + 2 * PL + off) = l;
@@ -184,7 +210,7 @@ __device__ __forceinline__ void store_tile(__bf16* __restrict__ lds, const Stage
   }
 }
 
-template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool VEC>
+template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool VEC, bool PIPE = true>
 __device__ __forceinline__ void mainloop(const float* __restrict__ A, long long lda, const float* __restrict__ B,
                                          long long ldb, int M, int N, int m0, int n0, int kbeg, int kend,
                                          __bf16* smem, floatx16 (&acc)[TBM / WM / 32][TBN / WN / 32]) {
@@ -221,10 +247,12 @@ __device__ __forceinline__ void mainloop(const float* __restrict__ A, long long 
       for (int pl = 0; pl < 3; ++pl) {
 #pragma unroll
         for (int i = 0; i < FM; ++i)
-          a[pl][i] = *reinterpret_cast<const bf16x8*>(as + pl * PA + slot_off<BK>(wm + 32 * i + cl, 2 * ks + h));
+          a[pl][i] = AK ? *reinterpret_cast<const bf16x8*>(as + pl * PA + slot_off<BK>(wm + 32 * i + cl, 2 * ks + h))
+                        : mn_frag<TBM>(as + pl * PA, wm + 32 * i, ks, lane);
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          b[pl][j] = *reinterpret_cast<const bf16x8*>(bs + pl * PB + slot_off<BK>(wn + 32 * j + cl, 2 * ks + h));
+          b[pl][j] = BK_ ? *reinterpret_cast<const bf16x8*>(bs + pl * PB + slot_off<BK>(wn + 32 * j + cl, 2 * ks + h))
+                         : mn_frag<TBN>(bs + pl * PB, wn + 32 * j, ks, lane);
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -240,40 +268,66 @@ __device__ __forceinline__ void mainloop(const float* __restrict__ A, long long 
         }
     }
   };
-  // Software pipeline, two register sets (unrolled by 2): during k-tile kt the LDS stage kt&1 is
-  // consumed by the MFMAs while the registers of tile kt+1 (loaded one iteration earlier, so their
-  // global latency is covered by a whole iteration) are split and written to the other stage in
-  // the same basic block, where the scheduler interleaves that VALU work with the MFMAs; tile
-  // kt+2 is loaded into the register set tile kt vacated.  Past the last full tile the loads
-  // re-read that tile (pointers stop advancing) and the spare stores hit an unread stage, so the
-  // steady state has no branches.
-  Stage<AK, TBM, BK, NT> ra1;
-  Stage<BK_, TBN, BK, NT> rb1;
-  if (nkf > 0) {
-    load_full<AK, TBM, BK, NT>(sa, lda, ra, nkf > 1);
-    load_full<BK_, TBN, BK, NT>(sb, ldb, rb, nkf > 1);
-    load_full<AK, TBM, BK, NT>(sa, lda, ra1, nkf > 2);
-    load_full<BK_, TBN, BK, NT>(sb, ldb, rb1, nkf > 2);
-    store_tile<AK, TBM, BK, NT>(smem, ra);
-    store_tile<BK_, TBN, BK, NT>(smem + 3 * PA, rb);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nkf; kt += 2) {
-    // even step: compute stage 0 | split ra1/rb1 (tile kt+1) -> stage 1 | load tile kt+2 -> ra/rb
-    load_full<AK, TBM, BK, NT>(sa, lda, ra, kt + 3 < nkf);
-    load_full<BK_, TBN, BK, NT>(sb, ldb, rb, kt + 3 < nkf);
-    compute(0);
-    store_tile<AK, TBM, BK, NT>(smem + BUF, ra1);
-    store_tile<BK_, TBN, BK, NT>(smem + BUF + 3 * PA, rb1);
+  if constexpr (!PIPE) {
+    // one register set: prefetch tile kt+1 while computing tile kt, write it after the MFMAs
+    // (fewer VGPRs: lets two 8-wave blocks share a CU)
+    if (nkf > 0) {
+      load_full<AK, TBM, BK, NT>(sa, lda, ra, nkf > 1);
+      load_full<BK_, TBN, BK, NT>(sb, ldb, rb, nkf > 1);
+      store_tile<AK, TBM, BK, NT>(smem, ra);
+      store_tile<BK_, TBN, BK, NT>(smem + 3 * PA, rb);
+    }
     __syncthreads();
-    if (kt + 1 >= nkf) break;
-    // odd step: compute stage 1 | split ra/rb (tile kt+2) -> stage 0 | load tile kt+3 -> ra1/rb1
-    load_full<AK, TBM, BK, NT>(sa, lda, ra1, kt + 4 < nkf);
-    load_full<BK_, TBN, BK, NT>(sb, ldb, rb1, kt + 4 < nkf);
-    compute(1);
-    store_tile<AK, TBM, BK, NT>(smem, ra);
-    store_tile<BK_, TBN, BK, NT>(smem + 3 * PA, rb);
+    for (int kt = 0; kt < nkf; ++kt) {
+      const int cur = kt & 1;
+      const bool more = kt + 1 < nkf;
+      if (more) {
+        load_full<AK, TBM, BK, NT>(sa, lda, ra, kt + 2 < nkf);
+        load_full<BK_, TBN, BK, NT>(sb, ldb, rb, kt + 2 < nkf);
+      }
+      compute(cur);
+      if (more) {
+        store_tile<AK, TBM, BK, NT>(smem + (cur ^ 1) * BUF, ra);
+        store_tile<BK_, TBN, BK, NT>(smem + (cur ^ 1) * BUF + 3 * PA, rb);
+      }
+      __syncthreads();
+    }
+  } else {
+    // Software pipeline, two register sets (unrolled by 2): during k-tile kt the LDS stage kt&1 is
+    // consumed by the MFMAs while the registers of tile kt+1 (loaded one iteration earlier, so their
+    // global latency is covered by a whole iteration) are split and written to the other stage in
+    // the same basic block, where the scheduler interleaves that VALU work with the MFMAs; tile
+    // kt+2 is loaded into the register set tile kt vacated.  Past the last full tile the loads
+    // re-read that tile (pointers stop advancing) and the spare stores hit an unread stage, so the
+    // steady state has no branches.
+    Stage<AK, TBM, BK, NT> ra1;
+    Stage<BK_, TBN, BK, NT> rb1;
+    if (nkf > 0) {
+      load_full<AK, TBM, BK, NT>(sa, lda, ra, nkf > 1);
+      load_full<BK_, TBN, BK, NT>(sb, ldb, rb, nkf > 1);
+      load_full<AK, TBM, BK, NT>(sa, lda, ra1, nkf > 2);
+      load_full<BK_, TBN, BK, NT>(sb, ldb, rb1, nkf > 2);
+      store_tile<AK, TBM, BK, NT>(smem, ra);
+      store_tile<BK_, TBN, BK, NT>(smem + 3 * PA, rb);
+    }
     __syncthreads();
+    for (int kt = 0; kt < nkf; kt += 2) {
+      // even step: compute stage 0 | split ra1/rb1 (tile kt+1) -> stage 1 | load tile kt+2 -> ra/rb
+      load_full<AK, TBM, BK, NT>(sa, lda, ra, kt + 3 < nkf);
+      load_full<BK_, TBN, BK, NT>(sb, ldb, rb, kt + 3 < nkf);
+      compute(0);
+      store_tile<AK, TBM, BK, NT>(smem + BUF, ra1);
+      store_tile<BK_, TBN, BK, NT>(smem + BUF + 3 * PA, rb1);
+      __syncthreads();
+      if (kt + 1 >= nkf) break;
+      // odd step: compute stage 1 | split ra/rb (tile kt+2) -> stage 0 | load tile kt+3 -> ra1/rb1
+      load_full<AK, TBM, BK, NT>(sa, lda, ra1, kt + 4 < nkf);
+      load_full<BK_, TBN, BK, NT>(sb, ldb, rb1, kt + 4 < nkf);
+      compute(1);
+      store_tile<AK, TBM, BK, NT>(smem, ra);
+      store_tile<BK_, TBN, BK, NT>(smem + 3 * PA, rb);
+      __syncthreads();
+    }
   }
   if (krem > 0) {  // peeled partial k-tile (masked loads); the pointers rest on the last full tile
     const int cur = nkf & 1;
@@ -291,7 +345,7 @@ __device__ __forceinline__ void mainloop(const float* __restrict__ A, long long 
   }
 }
 
-template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool VEC, int EPI, int OCC>
+template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool VEC, int EPI, int OCC, bool PIPE = true>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_x6_kernel(K3mGemm g) {
   constexpr int LDS_BF16 = 2 * 3 * (TBM + TBN) * BK;
   constexpr int EPI_F32 = WM * WN * 32 * (TBN / WN + 8);
@@ -306,7 +360,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_x6_kernel(K3mGemm g) {
     kend = min(g.k, kbeg + per);
   }
   floatx16 acc[TBM / WM / 32][TBN / WN / 32];
-  mainloop<TBM, TBN, WM, WN, BK, AK, BK_, VEC>(static_cast<const float*>(g.a), g.lda, static_cast<const float*>(g.b),
+  mainloop<TBM, TBN, WM, WN, BK, AK, BK_, VEC, PIPE>(static_cast<const float*>(g.a), g.lda, static_cast<const float*>(g.b),
                                                g.ldb, g.m, g.n, m0, n0, kbeg, kend, reinterpret_cast<__bf16*>(smem), acc);
   k3m_f32::epilogue<TBM, TBN, WM, WN, EPI, WORDS>(g, m0, n0, smem, acc);
 }

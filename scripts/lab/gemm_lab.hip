@@ -44,11 +44,11 @@ void launch(const K3mGemm& g, hipStream_t st) {
   hipLaunchKernelGGL((gemm_f32_kernel<TBM, TBN, WM, WN, AK, BK_, true, EPI, OCC>), grid, dim3(64 * WM * WN), 0, st, g);
 }
 
-template <int TBM, int TBN, int WM, int WN, int BK, int OCC, int EPI, bool AK, bool BK_>
+template <int TBM, int TBN, int WM, int WN, int BK, int OCC, int EPI, bool AK, bool BK_, bool PIPE = true>
 void launch_x6(const K3mGemm& g, hipStream_t st) {
   const int tm = (g.m + TBM - 1) / TBM, tn = (g.n + TBN - 1) / TBN;
   dim3 grid(tm * tn, g.splitk > 1 ? g.splitk : 1);
-  hipLaunchKernelGGL((k3m_x6::gemm_x6_kernel<TBM, TBN, WM, WN, BK, AK, BK_, true, EPI, OCC>), grid, dim3(64 * WM * WN), 0, st, g);
+  hipLaunchKernelGGL((k3m_x6::gemm_x6_kernel<TBM, TBN, WM, WN, BK, AK, BK_, true, EPI, OCC, PIPE>), grid, dim3(64 * WM * WN), 0, st, g);
 }
 
 // fp64 reference C = A.B^T (nt) for the accuracy check
@@ -77,8 +77,10 @@ std::vector<std::pair<std::string, Launcher>> variants() {
   return {
       {"x6 256x256 2x4 bk16", launch_x6<256, 256, 2, 4, 16, 1, EPI, AK, BK_>},
       {"x6 256x128 4x2 bk32", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_>},
-      {"x6 128x128 2x2 bk32", launch_x6<128, 128, 2, 2, 32, 1, EPI, AK, BK_>},
-      {"x6 64x64 2x2 bk16 o2", launch_x6<64, 64, 2, 2, 16, 2, EPI, AK, BK_>},
+      {"x6 256x128 bk16 2blk nopipe", launch_x6<256, 128, 4, 2, 16, 4, EPI, AK, BK_, false>},
+      {"x6 256x128 bk32 nopipe", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, false>},
+      {"x6 128x128 bk32 o1", launch_x6<128, 128, 2, 2, 32, 1, EPI, AK, BK_>},
+      {"x6 128x128 bk16 3blk nopipe", launch_x6<128, 128, 2, 2, 16, 3, EPI, AK, BK_, false>},
   };
 }
 
