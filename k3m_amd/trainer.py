@@ -80,6 +80,16 @@ class Trainer(object):
         fp.grad.zero_()
         self.global_step += 1
 
+    def save_checkpoint(self, tar_path=None, bin_path=None):
+        """The reference driver's .tar / .bin files (train_concap_struc.py:691-705; k3m_amd/checkpoint.py)."""
+        from .checkpoint import save_checkpoint
+        save_checkpoint(self, tar_path=tar_path, bin_path=bin_path)
+
+    def load_checkpoint(self, tar_path):
+        """Resume from a reference-layout .tar (train_concap_struc.py:277-293)."""
+        from .checkpoint import load_checkpoint
+        return load_checkpoint(self, tar_path)
+
     def step(self, batch, noise=None, ent_neg=None, val_neg=None):
         eng = self.engine
         out, ctx = eng.forward(batch, train=True, noise=noise, ent_neg=ent_neg, val_neg=val_neg,
