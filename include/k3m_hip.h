@@ -238,6 +238,17 @@ int k3m_convert(const void* x, int xdtype, void* y, int ydtype, long long n, int
                 hipStream_t stream);
 int k3m_add_inplace(void* y, const void* x, long long n, float alpha, int dtype, hipStream_t stream);
 
+/* ---- Data path ------------------------------------------------------
+ * Global-region collation of a batch of region features, fused with mask_region's feature
+ * zeroing: replaces the numpy block of ConceptCapLoaderTrain_struc.__iter__
+ * (vilbert_k3m/datasets/concept_cap_dataset_struc.py:381-388) and image_feat[i] = 0 (:913-915).
+ * feat fp32 [B][R][F] (sample stride ldb floats), zero_feat / masked_label uint8 [B][R] (from
+ * k3m_prep_regions, k3m_data.h); out fp32 [B][R+1][F]: row 0 = (float)((double)sum_r feat' / cnt),
+ * cnt = #(masked_label == 0) (0 -> 1), rows 1.. = feat' (masked rows zeroed).  Bit-identical to the
+ * reference's numpy (row-ordered fp32 sum, double division).  F % 4 == 0, 16-B aligned pointers. */
+int k3m_collate_regions(const float* feat, long long ldb, const uint8_t* zero_feat, const uint8_t* masked_label,
+                        int B, int R, int F, float* out, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

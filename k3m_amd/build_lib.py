@@ -7,7 +7,7 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libk3m_hip.so")
-SOURCES = ["gemm.hip", "gemm_bf16.hip", "norm.hip", "attention.hip", "attention_bf16.hip", "loss.hip", "fusion.hip", "struct.hip", "adamw.hip"]
+SOURCES = ["gemm.hip", "gemm_bf16.hip", "norm.hip", "attention.hip", "attention_bf16.hip", "loss.hip", "fusion.hip", "struct.hip", "adamw.hip", "data.hip"]
 FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-mcode-object-version=5", "-Wno-unused-result"]
 
 
@@ -48,5 +48,24 @@ def build(force=False, jobs=8, verbose=False):
     return OUT
 
 
+DATA_SRC = os.path.join(HERE, "host", "preprocess.cpp")
+DATA_OUT = os.path.join(HERE, "libk3m_data.so")
+# -ffp-contract=off: every fp32 expression rounds as the numpy array expression it restates
+DATA_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall"]
+
+
+def build_data(force=False):
+    """Build the host data-path library libk3m_data.so (plain g++, no GPU code)."""
+    hdr = os.path.join(os.path.dirname(HERE), "include", "k3m_data.h")
+    if not force and os.path.exists(DATA_OUT) and os.path.getmtime(DATA_OUT) >= max(
+            os.path.getmtime(DATA_SRC), os.path.getmtime(hdr)):
+        return DATA_OUT
+    r = subprocess.run(["g++"] + DATA_FLAGS + [DATA_SRC, "-o", DATA_OUT], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("g++ failed for %s:\n%s" % (DATA_SRC, r.stderr[-4000:]))
+    return DATA_OUT
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_data(force="--force" in sys.argv))

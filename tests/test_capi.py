@@ -26,3 +26,17 @@ def test_library_exports_every_symbol():
     assert sorted(got) == declared()
     lib = _lib.load()
     assert lib is not None
+
+
+def declared_data():
+    src = open(os.path.join(REPO, "include", "k3m_data.h")).read()
+    return sorted(set(re.findall(r"^(?:int|void|uint32_t|double|int64_t) (k3m_[a-z0-9_]+)\(", src, re.M)))
+
+
+def test_data_header_matches_library():
+    from k3m_amd import data
+    if not os.path.exists(data.DATA_LIB_PATH):
+        from k3m_amd.build_lib import build_data
+        build_data()
+    assert declared_data() == sorted(data.DATA_SIGNATURES)
+    assert sorted(data.data_exported_symbols()) == declared_data()
