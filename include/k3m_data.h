@@ -36,17 +36,19 @@ int64_t k3m_rng_randint_numpy(K3mRng* r, int64_t high);
  * mask_word :763-783): truncate the token ids to max_len-2, mask 15% of them (80% -> mask_id,
  * 10% -> np.random.randint(vocab), 10% kept; one py draw per token, an np draw for the 10% case),
  * add [CLS]=cls_id ... [SEP]=sep_id, pad to max_len.  Outputs are int64 [max_len].  visualization != 0
- * keeps the draws but masks nothing (the reference's visualization flag). */
+ * keeps the draws but masks nothing (the reference's visualization flag).  py == NULL: no draws and
+ * no masking (the fine-tuning K3MPreprocessBatch, dataset:1035-1038; np_rng may then be NULL). */
 int k3m_prep_text(const int32_t* tok, int ntok, int max_len, int mask_id, int cls_id, int sep_id, int vocab,
                   int visualization, K3mRng* py, K3mRng* np_rng, int64_t* input_ids, int64_t* input_mask, int64_t* segment_ids,
                   int64_t* lm_label_ids);
 
 /* Property-value text of one sample (mask_word_pv :815-840, index_pv :785-813): truncate to
- * max_len-2, mask every value token of triples 2..n (':'=colon_id ... ';'=semi_id), add
- * [CLS]/[SEP], pad; index_p/index_v int64 [max_num_pv][2] ([begin, ':' pos], [':' pos + 1, ';' pos]),
- * padded with [0, 0].  Deterministic. */
-int k3m_prep_pv(const int32_t* tok, int ntok, int max_len, int max_num_pv, int mask_id, int cls_id, int sep_id,
-                int colon_id, int semi_id, int64_t* input_ids, int64_t* input_mask, int64_t* segment_ids,
+ * max_len-2, mask every value token of triples 2..n (':'=colon_id ... ';'=semi_id) when
+ * mask_values != 0 (pretraining; 0 for fine-tuning, dataset:1036), add [CLS]/[SEP], pad;
+ * index_p/index_v int64 [max_num_pv][2] ([begin, ':' pos], [':' pos + 1, ';' pos]), padded with
+ * [0, 0].  Deterministic. */
+int k3m_prep_pv(const int32_t* tok, int ntok, int max_len, int max_num_pv, int mask_values, int mask_id, int cls_id,
+                int sep_id, int colon_id, int semi_id, int64_t* input_ids, int64_t* input_mask, int64_t* segment_ids,
                 int64_t* lm_label_ids, int64_t* index_p, int64_t* index_v);
 
 /* Regions of one sample (__call__ :575-610 + mask_region :898-933): box IoU, location
@@ -55,7 +57,8 @@ int k3m_prep_pv(const int32_t* tok, int ntok, int max_len, int max_num_pv, int m
  * masked boxes and every box overlapping one by IoU > 0.4 flagged in masked_label (they leave the
  * global-region mean).  num_boxes <= 0 takes the reference's default box.  Outputs over
  * max_region rows: image_loc fp32 [max_region][5], image_label / image_mask int64, zero_feat /
- * masked_label uint8.  The effective num_boxes is returned through nb_out. */
+ * masked_label uint8.  The effective num_boxes is returned through nb_out.  py == NULL: no region
+ * masking (K3MPreprocessBatch.image_processing, dataset:1180-1216). */
 int k3m_prep_regions(const float* boxes, int num_boxes, float image_h, float image_w, int max_region,
                      int visualization, K3mRng* py,
                      float* image_loc, int64_t* image_label, int64_t* image_mask, uint8_t* zero_feat,

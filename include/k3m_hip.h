@@ -229,6 +229,11 @@ int k3m_sa_gather_bwd(const float* dX, const int64_t* index_p, const int64_t* in
 int k3m_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, long long n, double lr, double beta1,
               double beta2, double eps, double wd, int step, float grad_scale, hipStream_t stream);
 
+/* torch.optim.AdamW (decoupled decay applied first, eps added after the bias correction of sqrt(v)):
+ * the optimizer of the fine-tuning driver (finetune.py:356-361).  Same arguments as k3m_adamw. */
+int k3m_adamw_torch(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, long long n, double lr,
+                    double beta1, double beta2, double eps, double wd, int step, float grad_scale, hipStream_t stream);
+
 /* Cast helpers for the mixed-precision path. */
 int k3m_cast_f32_bf16(const float* x, uint16_t* y, long long n, hipStream_t stream);
 /* y = (accumulate ? y : 0) + alpha * x with a type conversion (fp32 <-> bf16): the boundary between
@@ -238,6 +243,27 @@ int k3m_convert(const void* x, int xdtype, void* y, int ydtype, long long n, int
                 hipStream_t stream);
 int k3m_add_inplace(void* y, const void* x, long long n, float alpha, int dtype, hipStream_t stream);
 
+/* ---- Item alignment fine-tuning --------------------------------------
+ * K3MForItemAlignment.forward (vilbert_k3m.py:3379-3456) heads over the stacked pair embedding
+ * e = c_final [2B][H] (item 1 rows, then item 2 rows); forward and backward fused.
+ * pair_cat: x[b] = dropout_p([e[b] ; e[B+b]]) [B][2H] (ClassificationHead input, :2177);
+ * pair_cat_bwd writes de [2B][H] from dx [B][2H] with the same mask. */
+int k3m_align_pair_cat(const float* e, int B, int H, float p, uint64_t seed, uint64_t off, float* x,
+                       hipStream_t stream);
+int k3m_align_pair_cat_bwd(const float* dx, int B, int H, float p, uint64_t seed, uint64_t off, float* de,
+                           hipStream_t stream);
+/* "ce": u = classifier.dense(x) [B][H]; logits = out_proj(dropout_p(tanh(u))) (W [2][H], bias [2]),
+ * probs = softmax, loss = mean CE with labels (float, truncated to long as labels.to(torch.long)).
+ * Writes logits/probs [B][2], dlogits [B][2], loss_rows [B], loss [1], du [B][H]; ACCUMULATES the
+ * out_proj gradients into gW / gb. */
+int k3m_align_ce_fwd_bwd(const float* u, const float* W, const float* bias, const float* labels, int B, int H,
+                         float p, uint64_t seed, uint64_t off, float* logits, float* probs, float* dlogits,
+                         float* loss_rows, float* loss, float* du, float* gW, float* gb, hipStream_t stream);
+/* "cosine": loss = CosineEmbeddingLoss(margin)(e1, e2, 2*labels-1); probs[b] = (cos(e1_b, e1_b) + 1)/2;
+ * de [2B][H] = d loss / d e (written). */
+int k3m_align_cosine_fwd_bwd(const float* e, const float* labels, int B, int H, float margin, float* loss,
+                             float* probs, float* loss_rows, float* de, hipStream_t stream);
+
 /* ---- Data path ------------------------------------------------------
  * Global-region collation of a batch of region features, fused with mask_region's feature
  * zeroing: replaces the numpy block of ConceptCapLoaderTrain_struc.__iter__
@@ -245,9 +271,12 @@ int k3m_add_inplace(void* y, const void* x, long long n, float alpha, int dtype,
  * feat fp32 [B][R][F] (sample stride ldb floats), zero_feat / masked_label uint8 [B][R] (from
  * k3m_prep_regions, k3m_data.h); out fp32 [B][R+1][F]: row 0 = (float)((double)sum_r feat' / cnt),
  * cnt = #(masked_label == 0) (0 -> 1), rows 1.. = feat' (masked rows zeroed).  Bit-identical to the
- * reference's numpy (row-ordered fp32 sum, double division).  F % 4 == 0, 16-B aligned pointers. */
+ * reference's numpy (row-ordered fp32 sum, double division).  F % 4 == 0, 16-B aligned pointers.
+ * Fine-tuning collation (K3MDataLoader.post_process, dataset:265-292): divisor int32 [B] = the raw
+ * num_boxes (no 0 -> 1 fix: 0 gives inf / nan as numpy), zero_feat / masked_label may be NULL;
+ * divisor NULL selects the pretraining count above. */
 int k3m_collate_regions(const float* feat, long long ldb, const uint8_t* zero_feat, const uint8_t* masked_label,
-                        int B, int R, int F, float* out, hipStream_t stream);
+                        const int32_t* divisor, int B, int R, int F, float* out, hipStream_t stream);
 
 #ifdef __cplusplus
 }

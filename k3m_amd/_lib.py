@@ -69,7 +69,13 @@ SIGNATURES = {
     "k3m_cast_f32_bf16": [vp, vp, i64, vp],
     "k3m_convert": [vp, i32, vp, i32, i64, i32, f32, vp],
     "k3m_add_inplace": [vp, vp, i64, f32, i32, vp],
-    "k3m_collate_regions": [vp, i64, vp, vp, i32, i32, i32, vp, vp],
+    "k3m_collate_regions": [vp, i64, vp, vp, vp, i32, i32, i32, vp, vp],
+    "k3m_adamw_torch": [vp, vp, vp, vp, vp, i64, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double, i32, f32,
+                        vp],
+    "k3m_align_pair_cat": [vp, i32, i32, f32, u64, u64, vp, vp],
+    "k3m_align_pair_cat_bwd": [vp, i32, i32, f32, u64, u64, vp, vp],
+    "k3m_align_ce_fwd_bwd": [vp, vp, vp, vp, i32, i32, f32, u64, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+    "k3m_align_cosine_fwd_bwd": [vp, vp, i32, i32, f32, vp, vp, vp, vp, vp],
 }
 
 _lib = None

@@ -36,7 +36,8 @@ def model_state_dict(fp):
     sd = {}
     for name, _ in fp.spec:
         sd[name] = fp.p[name].detach().to("cpu", copy=True)
-    sd[DECODER_KEY] = sd[TIED_TO]
+    if "cls.predictions.bias" in fp.p:   # pretraining model: the tied MLM decoder
+        sd[DECODER_KEY] = sd[TIED_TO]
     return sd
 
 

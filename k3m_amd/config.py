@@ -117,3 +117,22 @@ def pretrain_config(path, with_coattention=True, if_pre_sampling=1, visual_targe
     cfg.if_pre_sampling = if_pre_sampling
     cfg.num_negative = num_negative
     return cfg
+
+
+def finetune_config(path, loss_type="ce", use_image=True, with_coattention=True, if_pre_sampling=1, visual_target=0,
+                    dynamic_attention=False, num_negative_image=255):
+    """Load a JSON config and apply the fine-tuning driver's mutations (finetune.py:1307-1322):
+    model "roberta" (whose embeddings behave as BERT's — BertEmbeddings.forward ignores the
+    position ids RobertaEmbeddings passes, vilbert_k3m.py:361-367, :394-408), loss_type, use_image."""
+    cfg = BertConfig.from_json_file(path)
+    cfg.v_target_size = 1601 if visual_target == 0 else 2048
+    cfg.visual_target = visual_target
+    cfg.model = "roberta"
+    cfg.use_image = use_image
+    cfg.with_coattention = with_coattention
+    cfg.dynamic_attention = dynamic_attention
+    cfg.if_pre_sampling = if_pre_sampling
+    cfg.num_negative_image = num_negative_image
+    cfg.loss_type = loss_type
+    cfg.task = "item_alignment"
+    return cfg

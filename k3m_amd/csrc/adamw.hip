@@ -42,7 +42,56 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   }
 }
 
+// torch.optim.AdamW (the fine-tuning optimizer, finetune.py:356-361), foreach-path op order:
+// p *= 1 - lr*wd; m = lerp(m, g, 1-b1); v = v*b2 + (1-b2) g g; p -= step_size * m / (sqrt(v)/sqrt(bc2) + eps)
+__global__ __launch_bounds__(256) void adamw_torch_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                          float* __restrict__ m, float* __restrict__ v,
+                                                          uint16_t* __restrict__ pb, long long n4, float omb1,
+                                                          float b2, float omb2, float eps, float step_size,
+                                                          float bc2_sqrt, float keep, float gscale) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    floatx4 pp = reinterpret_cast<floatx4*>(p)[i];
+    floatx4 gg = reinterpret_cast<const floatx4*>(g)[i];
+    floatx4 mm = reinterpret_cast<floatx4*>(m)[i];
+    floatx4 vv = reinterpret_cast<floatx4*>(v)[i];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float gr = gg[q] * gscale;
+      pp[q] = __fmul_rn(pp[q], keep);
+      mm[q] = __fadd_rn(mm[q], __fmul_rn(omb1, __fsub_rn(gr, mm[q])));
+      vv[q] = __fadd_rn(__fmul_rn(vv[q], b2), __fmul_rn(__fmul_rn(omb2, gr), gr));
+      const float denom = __fadd_rn(__fdiv_rn(sqrtf(vv[q]), bc2_sqrt), eps);
+      pp[q] = __fadd_rn(pp[q], __fmul_rn(-step_size, __fdiv_rn(mm[q], denom)));
+    }
+    reinterpret_cast<floatx4*>(p)[i] = pp;
+    reinterpret_cast<floatx4*>(m)[i] = mm;
+    reinterpret_cast<floatx4*>(v)[i] = vv;
+    if (pb) {
+      uint2 u;
+      u.x = (uint32_t)from_f<bf16_t>(pp[0]).x | ((uint32_t)from_f<bf16_t>(pp[1]).x << 16);
+      u.y = (uint32_t)from_f<bf16_t>(pp[2]).x | ((uint32_t)from_f<bf16_t>(pp[3]).x << 16);
+      reinterpret_cast<uint2*>(pb)[i] = u;
+    }
+  }
+}
+
 }  // namespace
+
+extern "C" int k3m_adamw_torch(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, long long n, double lr,
+                               double beta1, double beta2, double eps, double wd, int step, float grad_scale,
+                               hipStream_t st) {
+  K3M_ARG(p && g && m && v && n >= 0 && n % 4 == 0 && step >= 1);
+  K3M_ARG(((uintptr_t)p & 15) == 0 && ((uintptr_t)g & 15) == 0 && ((uintptr_t)m & 15) == 0 && ((uintptr_t)v & 15) == 0);
+  if (n == 0) return 0;
+  const double bc1 = 1.0 - std::pow(beta1, step), bc2 = 1.0 - std::pow(beta2, step);
+  const long long n4 = n / 4;
+  const int blocks = (int)std::min<long long>((n4 + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(adamw_torch_kernel, dim3(blocks), dim3(256), 0, st, p, g, m, v, p_bf16, n4, (float)(1.0 - beta1),
+                     (float)beta2, (float)(1.0 - beta2), (float)eps, (float)(lr / bc1), (float)std::sqrt(bc2),
+                     (float)(1.0 - lr * wd), grad_scale);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int k3m_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, long long n, double lr,
                          double beta1, double beta2, double eps, double wd, int step, float grad_scale, hipStream_t st) {

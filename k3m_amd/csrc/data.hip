@@ -18,13 +18,19 @@ constexpr int COLL_BATCH = 36;     // row loads in flight per lane (all 36 regio
 __global__ __launch_bounds__(COLL_THREADS) void collate_regions_kernel(const float* __restrict__ feat, long long ldb,
                                                                        const uint8_t* __restrict__ zero_feat,
                                                                        const uint8_t* __restrict__ masked_label,
+                                                                       const int32_t* __restrict__ divisor,
                                                                        int R, int F, float* __restrict__ out) {
   const int b = blockIdx.y;
-  const uint8_t* zf = zero_feat + (long long)b * R;
-  const uint8_t* ml = masked_label + (long long)b * R;
-  int c = 0;   // every lane counts (R is small; the flags are one cache line per sample)
-  for (int r = 0; r < R; ++r) c += ml[r] == 0;
-  const double cnt = (double)(c == 0 ? 1 : c);
+  const uint8_t* zf = zero_feat ? zero_feat + (long long)b * R : nullptr;
+  double cnt;
+  if (divisor) {
+    cnt = (double)divisor[b];   // num_boxes as given (0 -> inf / nan, as numpy)
+  } else {
+    const uint8_t* ml = masked_label + (long long)b * R;
+    int c = 0;   // every lane counts (R is small; the flags are one cache line per sample)
+    for (int r = 0; r < R; ++r) c += ml[r] == 0;
+    cnt = (double)(c == 0 ? 1 : c);
+  }
   const int f4 = blockIdx.x * COLL_THREADS + threadIdx.x;   // float4 column
   if (4 * f4 >= F) return;
   const float* src = feat + (long long)b * ldb + 4 * f4;
@@ -39,7 +45,7 @@ __global__ __launch_bounds__(COLL_THREADS) void collate_regions_kernel(const flo
     for (int j = 0; j < COLL_BATCH; ++j) {
       const int r = r0 + j;
       if (r < R) {
-        if (zf[r]) v[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (zf && zf[r]) v[j] = floatx4{0.f, 0.f, 0.f, 0.f};
         *reinterpret_cast<floatx4*>(dst + (long long)(r + 1) * F) = v[j];
 #pragma unroll
         for (int e = 0; e < 4; ++e) s[e] = r == 0 ? v[j][e] : __fadd_rn(s[e], v[j][e]);   // row order, fp32
@@ -55,12 +61,14 @@ __global__ __launch_bounds__(COLL_THREADS) void collate_regions_kernel(const flo
 }  // namespace
 
 extern "C" int k3m_collate_regions(const float* feat, long long ldb, const uint8_t* zero_feat,
-                                   const uint8_t* masked_label, int B, int R, int F, float* out, hipStream_t st) {
-  K3M_ARG(feat && zero_feat && masked_label && out && B >= 0 && R > 0 && F > 0 && F % 4 == 0 && ldb >= (long long)R * F);
+                                   const uint8_t* masked_label, const int32_t* divisor, int B, int R, int F, float* out,
+                                   hipStream_t st) {
+  K3M_ARG(feat && out && (masked_label || divisor) && B >= 0 && R > 0 && F > 0 && F % 4 == 0 && ldb >= (long long)R * F);
   K3M_ARG((reinterpret_cast<uintptr_t>(feat) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0 && ldb % 4 == 0);
   if (B == 0) return 0;
   dim3 grid((F / 4 + COLL_THREADS - 1) / COLL_THREADS, B);
-  hipLaunchKernelGGL(collate_regions_kernel, grid, dim3(COLL_THREADS), 0, st, feat, ldb, zero_feat, masked_label, R, F, out);
+  hipLaunchKernelGGL(collate_regions_kernel, grid, dim3(COLL_THREADS), 0, st, feat, ldb, zero_feat, masked_label, divisor,
+                     R, F, out);
   K3M_CHECK_LAUNCH();
   return 0;
 }

@@ -39,7 +39,8 @@ DATA_SIGNATURES = {
     "k3m_rng_random": (C.c_double, [_R]),
     "k3m_rng_randint_numpy": (C.c_int64, [_R, C.c_int64]),
     "k3m_prep_text": (C.c_int, [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _R, _R, _vp, _vp, _vp, _vp]),
-    "k3m_prep_pv": (C.c_int, [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "k3m_prep_pv": (C.c_int, [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
+                              _vp]),
     "k3m_prep_regions": (C.c_int, [_vp, _i32, _f32, _f32, _i32, _i32, _R, _vp, _vp, _vp, _vp, _vp, _vp]),
 }
 
@@ -160,7 +161,7 @@ class BertPreprocessBatch(object):
         outp = np.empty((4, P), np.int64)
         ip = np.empty((NPV, 2), np.int64)
         iv = np.empty((NPV, 2), np.int64)
-        rc = dl.k3m_prep_pv(_p(tokp), tokp.size, P, NPV, self.mask_id, self.cls_id, self.sep_id, 131, 132,
+        rc = dl.k3m_prep_pv(_p(tokp), tokp.size, P, NPV, 1, self.mask_id, self.cls_id, self.sep_id, 131, 132,
                             _p(outp[0]), _p(outp[1]), _p(outp[2]), _p(outp[3]), _p(ip), _p(iv))
         if rc:
             raise ValueError("k3m_prep_pv: bad arguments")
@@ -259,7 +260,7 @@ class RegionCollator(object):
         image_feat = t.empty((B, R + 1, F), dtype=t.float32, device=dev)
         if dev.type != "cuda":
             raise RuntimeError("RegionCollator runs the collation on the GPU (no CPU fallback)")
-        _lib.call("k3m_collate_regions", feat_d.data_ptr(), R * F, zero.data_ptr(), mlab.data_ptr(), B, R, F,
+        _lib.call("k3m_collate_regions", feat_d.data_ptr(), R * F, zero.data_ptr(), mlab.data_ptr(), None, B, R, F,
                   image_feat.data_ptr(), _lib.stream())
         loc = np.empty((B, R + 1, 5), np.float32)
         loc[:, 0] = (0, 0, 1, 1, 1)
@@ -304,3 +305,167 @@ class K3mPretrainLoader(object):
                 buf = []
         if buf:
             yield self.collate(buf)
+
+
+# ------------------------------------------------------------------------------------------------
+# Fine-tuning pairs: K3MPreprocessBatch (dataset:936-1263) and the
+# K3MDataLoader collation (:255-292).  Nothing is masked or drawn at random; the global region is
+# the sum of the region rows divided by the RAW num_boxes (0 -> inf / nan, as the reference).
+
+PAIR_TUPLE = ["label", "item_id_1", "input_ids_1", "input_mask_1", "segment_ids_1", "input_ids_pv_1",
+              "input_mask_pv_1", "segment_ids_pv_1", "index_p_1", "index_v_1", "num_boxes_1", "image_feat_1",
+              "image_loc_1", "image_target_1", "image_mask_1", "item_id_2", "input_ids_2", "input_mask_2",
+              "segment_ids_2", "input_ids_pv_2", "input_mask_pv_2", "segment_ids_pv_2", "index_p_2", "index_v_2",
+              "num_boxes_2", "image_feat_2", "image_loc_2", "image_target_2", "image_mask_2"]
+
+
+class PreparedItem(object):
+    __slots__ = ("item_id", "text", "pv", "index_p", "index_v", "image_loc", "image_mask", "num_boxes", "nb", "feat",
+                 "target")
+
+
+class K3MPreprocessBatch(object):
+    """Drop-in for the reference's fine-tuning ``K3MPreprocessBatch`` (dataset:936-1263): a record
+    ``(label, item 1: item_id, caption, pv, category, image_h, image_w, num_boxes, boxes, features,
+    targets, item 2: ...)`` -> the reference's 29-tuple of numpy arrays."""
+
+    def __init__(self, tokenizer, max_seq_len=32, max_seq_len_pv=32, max_num_pv=20, max_region_len=36,
+                 v_feature_size=2048, v_target_size=1601, v_loc_size=5, visual_target=0):
+        if v_loc_size != 5:
+            raise ValueError("v_loc_size must be 5 (the reference's location layout)")
+        self.max_seq_len, self.max_seq_len_pv, self.max_num_pv = max_seq_len, max_seq_len_pv, max_num_pv
+        self.max_region_len, self.v_feature_size, self.v_target_size = max_region_len, v_feature_size, v_target_size
+        self.v_loc_size, self.visual_target, self.tokenizer = v_loc_size, visual_target, tokenizer
+        self.mask_id = int(tokenizer.convert_tokens_to_ids(tokenizer.mask_token))
+        sp = list(tokenizer.add_special_tokens_single_sentence([]))
+        if len(sp) != 2:
+            raise ValueError("tokenizer must wrap a sentence as [CLS] ids [SEP]")
+        self.cls_id, self.sep_id = int(sp[0]), int(sp[1])
+        self._dl = load_data_lib()
+
+    def prepare_item(self, item):
+        item_id, caption, pv, _category, image_h, image_w, num_boxes, boxes, feats, targets = item
+        dl, R = self._dl, self.max_region_len
+        s = PreparedItem()
+        s.item_id = item_id
+        tok = np.ascontiguousarray(self.tokenizer.encode(caption), dtype=np.int32)
+        T, P, NPV = self.max_seq_len, self.max_seq_len_pv, self.max_num_pv
+        s.text = np.empty((3, T), np.int64)
+        lab = np.empty(T, np.int64)
+        if dl.k3m_prep_text(_p(tok), tok.size, T, self.mask_id, self.cls_id, self.sep_id, 0, 0, None, None,
+                            _p(s.text[0]), _p(s.text[1]), _p(s.text[2]), _p(lab)):
+            raise ValueError("k3m_prep_text: bad arguments")
+        tokp = np.ascontiguousarray(self.tokenizer.encode(pv), dtype=np.int32)
+        s.pv = np.empty((3, P), np.int64)
+        labp = np.empty(P, np.int64)
+        s.index_p = np.empty((NPV, 2), np.int64)
+        s.index_v = np.empty((NPV, 2), np.int64)
+        if dl.k3m_prep_pv(_p(tokp), tokp.size, P, NPV, 0, self.mask_id, self.cls_id, self.sep_id, 131, 132,
+                          _p(s.pv[0]), _p(s.pv[1]), _p(s.pv[2]), _p(labp), _p(s.index_p), _p(s.index_v)):
+            raise ValueError("k3m_prep_pv: bad arguments")
+        nb = int(num_boxes)
+        if nb > R:
+            raise ValueError("num_boxes %d exceeds max_region_len %d" % (nb, R))
+        bx = np.ascontiguousarray(boxes, dtype=np.float32).reshape(-1, 4) if nb > 0 else np.zeros((0, 4), np.float32)
+        s.image_loc = np.empty((R, 5), np.float32)
+        il, im = np.empty(R, np.int64), np.empty(R, np.int64)
+        zf, ml = np.empty(R, np.uint8), np.empty(R, np.uint8)
+        nbo = C.c_int(0)
+        if dl.k3m_prep_regions(_p(bx), nb, float(image_h), float(image_w), R, 0, None, _p(s.image_loc), _p(il),
+                               _p(im), _p(zf), _p(ml), C.byref(nbo)):
+            raise ValueError("k3m_prep_regions: bad arguments")
+        s.num_boxes = num_boxes                      # raw, as InputExample(num_boxes=...) keeps it
+        s.nb = nbo.value
+        s.image_mask = (np.arange(R) < nb).astype(np.int64)   # [1] * num_boxes (raw) padded (:1148)
+        if nb > 0:
+            s.feat = np.asarray(feats, dtype=np.float32).reshape(nb, self.v_feature_size)
+            s.target = np.asarray(targets, dtype=np.float32).reshape(nb, self.v_target_size)
+        else:
+            s.feat = np.zeros((1, self.v_feature_size), np.float32)
+            s.target = np.zeros((1, self.v_target_size), np.float32)
+        return s
+
+    def prepare(self, data):
+        return data[0], self.prepare_item(data[1:11]), self.prepare_item(data[11:21])
+
+    def _item_tuple(self, s):
+        R = self.max_region_len
+        feat = np.zeros((R, self.v_feature_size), np.float32)
+        feat[:s.nb] = s.feat
+        if self.visual_target == 0:
+            target = np.zeros((R, self.v_target_size), np.float32)
+            target[:s.nb] = s.target
+        else:
+            target = feat.copy()
+        return (s.item_id, s.text[0], s.text[1], s.text[2], s.pv[0], s.pv[1], s.pv[2], s.index_p, s.index_v,
+                s.num_boxes, feat, s.image_loc, target, s.image_mask)
+
+    def __call__(self, data):
+        label, a, b = self.prepare(data)
+        return (label,) + self._item_tuple(a) + self._item_tuple(b)
+
+
+class PairCollator(object):
+    """K3MDataLoader.__iter__ collation (dataset:255-263, post_process :265-292) with the feature
+    rows collated on the GPU: returns the K3MForItemAlignment.forward arguments as a dict (plus
+    image_target_1/2, as the reference's batch carries them) and the item-id lists."""
+
+    def __init__(self, device, max_region_len=36, v_feature_size=2048, v_target_size=1601, visual_target=0):
+        import torch
+        self.torch = torch
+        self.device = torch.device(device)
+        self.R, self.F, self.Ct = max_region_len, v_feature_size, v_target_size
+        self.visual_target = visual_target
+
+    def _item(self, items):
+        from . import _lib
+        t = self.torch
+        B, R, F = len(items), self.R, self.F
+        if self.device.type != "cuda":
+            raise RuntimeError("PairCollator runs the collation on the GPU (no CPU fallback)")
+        pin = True
+        fh = t.zeros((B, R, F), dtype=t.float32, pin_memory=pin)
+        ct = F if self.visual_target else self.Ct
+        th = t.zeros((B, R, ct), dtype=t.float32, pin_memory=pin)
+        fn, tn = fh.numpy(), th.numpy()
+        for b, s in enumerate(items):
+            fn[b, :s.nb] = s.feat
+            if self.visual_target == 0:
+                tn[b, :s.nb] = s.target
+        dev = self.device
+        feat_d = fh.to(dev, non_blocking=True)
+        tgt = feat_d.clone() if self.visual_target else th.to(dev, non_blocking=True)
+        div = t.from_numpy(np.array([int(s.num_boxes) for s in items], np.int32)).to(dev, non_blocking=True)
+        out = t.empty((B, R + 1, F), dtype=t.float32, device=dev)
+        _lib.call("k3m_collate_regions", feat_d.data_ptr(), R * F, None, None, div.data_ptr(), B, R, F, out.data_ptr(),
+                  _lib.stream())
+        loc = np.empty((B, R + 1, 5), np.float32)
+        loc[:, 0] = (0, 0, 1, 1, 1)
+        loc[:, 1:] = np.stack([s.image_loc for s in items])
+        mask = np.ones((B, R + 1), np.int64)
+        mask[:, 1:] = np.stack([s.image_mask for s in items])
+        text = np.stack([s.text for s in items])
+        pv = np.stack([s.pv for s in items])
+
+        def d(a):
+            return t.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)
+
+        return dict(input_ids=d(text[:, 0]), attention_mask=d(text[:, 1]), token_type_ids=d(text[:, 2]),
+                    input_ids_pv=d(pv[:, 0]), attention_mask_pv=d(pv[:, 1]), token_type_ids_pv=d(pv[:, 2]),
+                    index_p=d(np.stack([s.index_p for s in items])), index_v=d(np.stack([s.index_v for s in items])),
+                    image_feat=out, image_loc=d(loc), image_attention_mask=d(mask), image_target=tgt), \
+            [s.item_id for s in items], (feat_d, div)
+
+    def __call__(self, prepared):
+        t = self.torch
+        labels = t.tensor(np.array([float(p[0]) for p in prepared], np.float32)).to(self.device)
+        out = {"labels": labels}
+        ids = []
+        keep = []
+        for k in (1, 2):
+            d, iid, hold = self._item([p[k] for p in prepared])
+            out.update({"%s_%d" % (n, k): v for n, v in d.items()})
+            ids.append(iid)
+            keep.append(hold)
+        self._hold = keep          # staging buffers stay alive until the next call
+        return out, ids[0], ids[1]

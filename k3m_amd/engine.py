@@ -102,7 +102,8 @@ class FlatParams(object):
         sd = {}
         for name, _ in self.spec:
             sd[name] = self.p[name]
-        sd["cls.predictions.decoder.weight"] = self.p["embeddings.word_embeddings.weight"]
+        if "cls.predictions.bias" in self.p:   # the tied MLM decoder of the pretraining model
+            sd["cls.predictions.decoder.weight"] = self.p["embeddings.word_embeddings.weight"]
         return sd
 
 
@@ -343,7 +344,7 @@ class K3MEngine(object):
         c = cfg
         assert getattr(c, "fixed_t_layer", 0) == 0 and getattr(c, "fixed_v_layer", 0) == 0
         assert not getattr(c, "in_batch_pairs", False) and not getattr(c, "fast_mode", False)
-        assert not getattr(c, "dynamic_attention", False) and getattr(c, "model", "bert") == "bert"
+        assert not getattr(c, "dynamic_attention", False) and getattr(c, "model", "bert") in ("bert", "roberta")
         assert getattr(c, "use_image", True) and c.with_coattention
         assert getattr(c, "visual_target", 0) == 0
         self.H, self.Hv, self.Hb = c.hidden_size, c.v_hidden_size, c.bi_hidden_size
@@ -370,11 +371,15 @@ class K3MEngine(object):
         self.gate = {m: Lin(fp, ["score_self_%s" % m, "score_cross1_%s" % m, "score_cross2_%s" % m])
                      for m in ("v", "t", "pv")}
         self.map_b2i = Lin(fp, "map_bi_to_individual")
-        self.mlm_t = Lin(fp, "cls.predictions.transform.dense")
-        self.mlm_ln = LN(fp, "cls.predictions.transform.LayerNorm")
-        self.img_t = Lin(fp, "cls.imagePredictions.transform.dense")
-        self.img_ln = LN(fp, "cls.imagePredictions.transform.LayerNorm")
-        self.img_dec = Lin(fp, "cls.imagePredictions.decoder")
+        # "pretrain": the pretraining heads + LPM; "item_alignment": the encoder up to c_final only
+        # (K3MForItemAlignment.item_embedding, vilbert_k3m.py:3329-3377; its pair head is k3m_amd.finetune)
+        self.task = getattr(c, "task", "pretrain")
+        if self.task == "pretrain":
+            self.mlm_t = Lin(fp, "cls.predictions.transform.dense")
+            self.mlm_ln = LN(fp, "cls.predictions.transform.LayerNorm")
+            self.img_t = Lin(fp, "cls.imagePredictions.transform.dense")
+            self.img_ln = LN(fp, "cls.imagePredictions.transform.LayerNorm")
+            self.img_dec = Lin(fp, "cls.imagePredictions.decoder")
         self.sw1, self.sw3 = Lin(fp, "struc_w1"), Lin(fp, "struc_w3")
         self.schedule = self._schedule()
 
@@ -402,11 +407,14 @@ class K3MEngine(object):
         return sch
 
     # ------------------------------------------------------------ forward
-    def forward(self, batch, train=True, noise=None, ent_neg=None, val_neg=None, seed=None):
+    def forward(self, batch, train=True, noise=None, ent_neg=None, val_neg=None, seed=None, groups=1):
         """Runs the forward of the step; returns (losses dict of device tensors, ctx for backward).
 
         batch: dict of device tensors with the reference names (A0 in SURVEY.md §8(a)).
-        noise: optional {v,t,pv: [B, L, 3, D]} gumbel noise; ent_neg/val_neg optional [B,NPV,2]."""
+        noise: optional {v,t,pv: [B, L, 3, D]} gumbel noise; ent_neg/val_neg optional [B,NPV,2].
+        groups: the batch is that many independent model calls stacked along dim 0 (the item
+        alignment pair: item 1 rows then item 2 rows); only the structure aggregator's
+        zero-triple fallback crosses items, and it is kept inside each group."""
         c = self.cfg
         fp = self.fp
         fp.refresh_shadow()
@@ -558,16 +566,31 @@ class K3MEngine(object):
         X = torch.empty((B * NPV, 3 * H), dtype=torch.float32, device=dev)
         nvalid = torch.empty((B,), dtype=torch.int32, device=dev)
         src = torch.empty((B,), dtype=torch.int32, device=dev)
-        L.call("k3m_sa_gather", seq_tp[BT:].data_ptr(), index_p.data_ptr(), index_v.data_ptr(), c_init.data_ptr(),
-               X.data_ptr(), nvalid.data_ptr(), src.data_ptr(), B, P, NPV, H, L.F32, L.stream())
+        assert B % groups == 0
+        Bg = B // groups
+        for gi in range(groups):   # src (zero-triple fallback) is group-relative
+            r0 = gi * Bg
+            L.call("k3m_sa_gather", seq_tp[BT + r0 * P:].data_ptr(), index_p[r0:].data_ptr(), index_v[r0:].data_ptr(),
+                   c_init[r0:].data_ptr(), X[r0 * NPV:].data_ptr(), nvalid[r0:].data_ptr(), src[r0:].data_ptr(), Bg, P,
+                   NPV, H, L.F32, L.stream())
         Tm = self.sw1.fwd(X)
         att = torch.empty((B, NPV), dtype=torch.float32, device=dev)
         agg = torch.empty((B, H), dtype=torch.float32, device=dev)
-        L.call("k3m_sa_attn_fwd", Tm.data_ptr(), nvalid.data_ptr(), src.data_ptr(), fp.p["struc_w2.weight"].data_ptr(),
-               fp.p["struc_w2.bias"].data_ptr(), c_init.data_ptr(), att.data_ptr(), agg.data_ptr(), B, NPV, H,
-               L.stream())
+        for gi in range(groups):
+            r0 = gi * Bg
+            L.call("k3m_sa_attn_fwd", Tm[r0 * NPV:].data_ptr(), nvalid[r0:].data_ptr(), src[r0:].data_ptr(),
+                   fp.p["struc_w2.weight"].data_ptr(), fp.p["struc_w2.bias"].data_ptr(), c_init[r0:].data_ptr(),
+                   att[r0:].data_ptr(), agg[r0:].data_ptr(), Bg, NPV, H, L.stream())
         c_final = c_init.clone()
         self.sw3.fwd(agg, out=c_final, beta=1.0)
+        if self.task != "pretrain":
+            ctx["struct"] = (X, nvalid, src, Tm, att, agg, c_init, c_final, None, None, None, index_p, index_v, NPV,
+                             None)
+            ctx["groups"] = groups
+            ctx["batch"] = batch
+            return {"c_initial": c_init, "c_final": c_final, "pooled_t": pooled_t, "pooled_pv": pooled_pv,
+                    "pooled_v": pooled_v}, ctx
+        assert groups == 1
         if ent_neg is None:
             ent_neg = torch.empty((B, NPV, 2), dtype=torch.int64, device=dev)
             val_neg = torch.empty((B, NPV, 2), dtype=torch.int64, device=dev)
@@ -682,7 +705,7 @@ class K3MEngine(object):
         dseq_v = torch.zeros_like(seq_v)
 
         # ---- MLM head (dlogits already in place from the forward CE kernel)
-        idx_m, n_m, hm, pre_m, hl, xh_m, rs_m, dlog = ctx["mlm"]
+        idx_m, n_m, hm, pre_m, hl, xh_m, rs_m, dlog = ctx["mlm"] if "mlm" in ctx else (None, 0) + (None,) * 6
         if n_m:
             bf = self.dtype == "bf16"
             E = fp.p16("embeddings.word_embeddings.weight") if bf else fp.p["embeddings.word_embeddings.weight"]
@@ -698,7 +721,7 @@ class K3MEngine(object):
             self.mlm_t.wgrad(du, hm)
             dhm = self.mlm_t.dgrad(du)
             ops.scatter_add_rows(dhm, idx_m, n_m, dseq_tp)
-        idx_v, n_v, hv, pre_v, hlv, xh_iv, rs_iv, dlv = ctx["img"]
+        idx_v, n_v, hv, pre_v, hlv, xh_iv, rs_iv, dlv = ctx["img"] if "img" in ctx else (None, 0) + (None,) * 6
         if n_v:
             dhlv = self.img_dec.dgrad(dlv, alpha=w_img)
             self.img_dec.wgrad(dlv, hlv, alpha=w_img)
@@ -715,11 +738,12 @@ class K3MEngine(object):
          margin) = ctx["struct"]
         dcf = torch.zeros_like(c_final)
         dX = torch.zeros_like(X)
-        L.call("k3m_lpm_bwd", c_final.data_ptr(), X.data_ptr(), nvalid.data_ptr(), ent_neg.data_ptr(),
-               val_neg.data_ptr(), B, NPV, H, margin, lws.data_ptr(), dcf.data_ptr(), dX.data_ptr(), L.stream())
-        if w_lpm != 1.0:
-            ops.add_(dcf, dcf.clone(), w_lpm - 1.0)
-            ops.add_(dX, dX.clone(), w_lpm - 1.0)
+        if lws is not None:
+            L.call("k3m_lpm_bwd", c_final.data_ptr(), X.data_ptr(), nvalid.data_ptr(), ent_neg.data_ptr(),
+                   val_neg.data_ptr(), B, NPV, H, margin, lws.data_ptr(), dcf.data_ptr(), dX.data_ptr(), L.stream())
+            if w_lpm != 1.0:
+                ops.add_(dcf, dcf.clone(), w_lpm - 1.0)
+                ops.add_(dX, dX.clone(), w_lpm - 1.0)
         if "d_c_final" in ctx:
             ops.add_(dcf, ctx["d_c_final"].contiguous())
         dagg = self.sw3.dgrad(dcf)
@@ -728,9 +752,14 @@ class K3MEngine(object):
         if "d_c_initial" in ctx:
             ops.add_(dci, ctx["d_c_initial"].contiguous())
         dT = torch.zeros_like(Tm)
-        L.call("k3m_sa_attn_bwd", dagg.data_ptr(), Tm.data_ptr(), att.data_ptr(), nvalid.data_ptr(), src.data_ptr(),
-               fp.p["struc_w2.weight"].data_ptr(), dT.data_ptr(), fp.g["struc_w2.weight"].data_ptr(),
-               fp.g["struc_w2.bias"].data_ptr(), dci.data_ptr(), B, NPV, H, L.stream())
+        groups = ctx.get("groups", 1)
+        Bg = B // groups
+        for gi in range(groups):
+            r0 = gi * Bg
+            L.call("k3m_sa_attn_bwd", dagg[r0:].data_ptr(), Tm[r0 * NPV:].data_ptr(), att[r0:].data_ptr(),
+                   nvalid[r0:].data_ptr(), src[r0:].data_ptr(), fp.p["struc_w2.weight"].data_ptr(),
+                   dT[r0 * NPV:].data_ptr(), fp.g["struc_w2.weight"].data_ptr(), fp.g["struc_w2.bias"].data_ptr(),
+                   dci[r0:].data_ptr(), Bg, NPV, H, L.stream())
         self.sw1.wgrad(dT, X)
         self.sw1.dgrad(dT, dx=dX, beta=1.0)
         L.call("k3m_sa_gather_bwd", dX.data_ptr(), index_p.data_ptr(), index_v.data_ptr(), nvalid.data_ptr(),

@@ -114,14 +114,14 @@ int64_t k3m_rng_randint_numpy(K3mRng* r, int64_t high) {
 int k3m_prep_text(const int32_t* tok, int ntok, int max_len, int mask_id, int cls_id, int sep_id, int vocab,
                   int visualization, K3mRng* py, K3mRng* np_rng, int64_t* input_ids, int64_t* input_mask, int64_t* segment_ids,
                   int64_t* lm_label_ids) {
-  if (max_len < 2 || ntok < 0 || (ntok > 0 && !tok) || !py || !np_rng) return 1;
+  if (max_len < 2 || ntok < 0 || (ntok > 0 && !tok) || (py && !np_rng)) return 1;
   const int n = ntok < max_len - 2 ? ntok : max_len - 2;   // _truncate_seq_pair (:741-753)
   input_ids[0] = cls_id;
   lm_label_ids[0] = -1;
   for (int i = 0; i < n; ++i) {                            // mask_word (:763-783)
     const int32_t t = tok[i];
-    double prob = k3m_rng_random(py);
     int64_t out = t, lab = -1;
+    double prob = py ? k3m_rng_random(py) : 1.0;   // no stream: no masking (K3MPreprocessBatch)
     if (prob < 0.15 && !visualization) {
       prob /= 0.15;
       if (prob < 0.8) out = mask_id;
@@ -144,8 +144,8 @@ int k3m_prep_text(const int32_t* tok, int ntok, int max_len, int mask_id, int cl
   return 0;
 }
 
-int k3m_prep_pv(const int32_t* tok, int ntok, int max_len, int max_num_pv, int mask_id, int cls_id, int sep_id,
-                int colon_id, int semi_id, int64_t* input_ids, int64_t* input_mask, int64_t* segment_ids,
+int k3m_prep_pv(const int32_t* tok, int ntok, int max_len, int max_num_pv, int mask_values, int mask_id, int cls_id,
+                int sep_id, int colon_id, int semi_id, int64_t* input_ids, int64_t* input_mask, int64_t* segment_ids,
                 int64_t* lm_label_ids, int64_t* index_p, int64_t* index_v) {
   if (max_len < 2 || max_len > 4096 || ntok < 0 || (ntok > 0 && !tok) || max_num_pv < 0) return 1;
   const int n = ntok < max_len - 2 ? ntok : max_len - 2;
@@ -162,7 +162,7 @@ int k3m_prep_pv(const int32_t* tok, int ntok, int max_len, int max_num_pv, int m
     input_ids[1 + i] = tok[i];
     lm_label_ids[1 + i] = -1;
   }
-  const int npair = (n131 - off) < (n132 - off) ? (n131 - off) : (n132 - off);
+  const int npair = !mask_values ? 0 : (n131 - off) < (n132 - off) ? (n131 - off) : (n132 - off);
   for (int p = 0; p < npair; ++p) {
     const int beg = i131[p + off], end = i132[p + off];
     for (int i = beg + 1; i < end; ++i) {
@@ -212,7 +212,7 @@ int k3m_prep_regions(const float* boxes, int num_boxes, float image_h, float ima
                      int visualization, K3mRng* py,
                      float* image_loc, int64_t* image_label, int64_t* image_mask, uint8_t* zero_feat,
                      uint8_t* masked_label, int* nb_out) {
-  if (max_region <= 0 || !py || (num_boxes > 0 && !boxes) || num_boxes > max_region) return 1;
+  if (max_region <= 0 || (num_boxes > 0 && !boxes) || num_boxes > max_region) return 1;
   const float defbox[4] = {0.1f, 0.1f, (float)(800.0 - 0.1), (float)(800.0 - 0.1)};
   const float* b = boxes;
   int nb = num_boxes;
@@ -242,7 +242,7 @@ int k3m_prep_regions(const float* boxes, int num_boxes, float image_h, float ima
     image_label[i] = -1;
     image_mask[i] = i < nb ? 1 : 0;
   }
-  for (int i = 0; i < nb; ++i) {   // mask_region (:898-933)
+  for (int i = 0; py && i < nb; ++i) {   // mask_region (:898-933); no stream: no masking
     double prob = k3m_rng_random(py);
     if (prob < 0.15 && !visualization) {
       prob /= 0.15;

@@ -64,7 +64,11 @@ def _conn_layer(p, H1, H2, Hb, I1, I2):
 
 
 def param_spec(cfg):
-    """Ordered [(name, shape)] exactly as the reference ``named_parameters()``."""
+    """Ordered [(name, shape)] exactly as the reference ``named_parameters()``; ``cfg.task``
+    selects the model: "pretrain" (BertForMultiModalPreTraining_tri_stru, default) or
+    "item_alignment" (K3MForItemAlignment, vilbert_k3m.py:2862-2950)."""
+    if getattr(cfg, "task", "pretrain") == "item_alignment":
+        return item_alignment_spec(cfg)
     H, I, V = cfg.hidden_size, cfg.intermediate_size, cfg.vocab_size
     Hv, Iv, Hb = cfg.v_hidden_size, cfg.v_intermediate_size, cfg.bi_hidden_size
     use_image = getattr(cfg, "use_image", True)
@@ -113,12 +117,64 @@ def param_spec(cfg):
     return s
 
 
+def _encoder_spec(cfg):
+    H, I = cfg.hidden_size, cfg.intermediate_size
+    Hv, Iv, Hb = cfg.v_hidden_size, cfg.v_intermediate_size, cfg.bi_hidden_size
+    nco = len(cfg.v_biattention_id)
+    s = []
+    for i in range(cfg.num_hidden_layers):
+        s += _bert_layer("encoder.layer.%d" % i, H, I)
+    for i in range(cfg.v_num_hidden_layers):
+        s += _bert_layer("encoder.v_layer.%d" % i, Hv, Iv)
+    if cfg.with_coattention:
+        for i in range(nco):
+            s += _conn_layer("encoder.c_layer.%d" % i, Hv, H, Hb, Iv, I)
+        for i in range(nco):
+            s += _conn_layer("encoder.c_layer_pv_v.%d" % i, Hv, H, Hb, Iv, I)
+        for i in range(nco):
+            s += _conn_layer("encoder.c_layer_pv_t.%d" % i, H, H, H, I, I)
+    return s
+
+
+def item_alignment_spec(cfg):
+    """K3MForItemAlignment.named_parameters() (vilbert_k3m.py:2866-2950, use_image=True): module
+    registration order embeddings, v_embeddings, v_pooler, encoder, t_pooler, the fusion maps and
+    gates, classifier (loss_type "ce": ClassificationHead :2164-2183), struc_w1..3."""
+    if not getattr(cfg, "use_image", True):
+        raise NotImplementedError("item alignment without the image modality (use_image=False)")
+    H, V = cfg.hidden_size, cfg.vocab_size
+    Hv, Hb = cfg.v_hidden_size, cfg.bi_hidden_size
+    s = [("embeddings.word_embeddings.weight", (V, H)),
+         ("embeddings.position_embeddings.weight", (cfg.max_position_embeddings, H)),
+         ("embeddings.token_type_embeddings.weight", (cfg.type_vocab_size, H))]
+    s += _ln("embeddings.LayerNorm", H)
+    s += _lin("v_embeddings.image_embeddings", Hv, cfg.v_feature_size)
+    s += _lin("v_embeddings.image_location_embeddings", Hv, 5)
+    s += _ln("v_embeddings.LayerNorm", Hv)
+    s += _lin("v_pooler.dense", Hb, Hv)
+    s += _encoder_spec(cfg)
+    s += _lin("t_pooler.dense", Hb, H)
+    s += _lin("map_individual_to_bi", Hb, H)
+    s += _lin("map_bi_to_individual", H, Hb)
+    for n in ("score_self_v", "score_cross1_v", "score_cross2_v", "soft_v"):
+        s += _lin(n, Hb, 3 * Hb)
+    for n in ("score_self_t", "score_cross1_t", "score_cross2_t", "soft_t",
+              "score_self_pv", "score_cross1_pv", "score_cross2_pv", "soft_pv"):
+        s += _lin(n, H, 3 * H)
+    if getattr(cfg, "loss_type", "ce") == "ce":
+        s += _lin("classifier.dense", H, 2 * H) + _lin("classifier.out_proj", 2, H)
+    s += _lin("struc_w1", H, 3 * H) + _lin("struc_w2", 1, H) + _lin("struc_w3", H, H)
+    return s
+
+
 _FROZEN_RE = re.compile(r"(\.q_dense[12]\.|^t_pooler\.|^v_pooler\.|^cls\.seq_relationship\.|"
                         r"^map_individual_to_bi\.|^soft_(v|t|pv)\.)")
 
 
 def is_frozen(name):
-    """True for the tensors that never get a gradient in the pretraining step."""
+    """True for the tensors that never get a gradient in the pretraining step (and, the same set
+    minus the absent NSP head, in the item-alignment step: its poolers, q_dense*,
+    map_individual_to_bi and soft_* outputs are unused too, vilbert_k3m.py:3183-3376)."""
     return bool(_FROZEN_RE.search(name))
 
 

@@ -38,6 +38,8 @@ def init_reference(fp, cfg, seed):
 
 
 class Trainer(object):
+    ADAMW = "k3m_adamw"   # pytorch_transformers AdamW (train_concap_struc.py:436-441)
+
     def __init__(self, cfg, device, lr=1e-4, warmup_steps=0, total_steps=10000, seed=1234, ddp=None,
                  loss_img_weight=1.0, beta1=0.9, beta2=0.98, eps=1e-8, weight_decay=0.01, init=True, dtype="fp32"):
         self.engine = K3MEngine(cfg, device, seed=seed, dtype=dtype)
@@ -73,7 +75,7 @@ class Trainer(object):
                 continue
             # with a bf16 encoder the same launch refreshes the weight shadow from the new fp32 values
             sh = fp.data16[off:].data_ptr() if fp.data16 is not None else None
-            L.call("k3m_adamw", fp.data[off:].data_ptr(), fp.grad[off:].data_ptr(), self.m[off:].data_ptr(),
+            L.call(self.ADAMW, fp.data[off:].data_ptr(), fp.grad[off:].data_ptr(), self.m[off:].data_ptr(),
                    self.v[off:].data_ptr(), sh, n, lr, self.beta1, self.beta2, self.eps, wd, step, grad_scale,
                    L.stream())
         fp.shadow_fresh = fresh   # frozen tensors are not updated: the shadow stays as fresh as it was

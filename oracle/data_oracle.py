@@ -27,3 +27,14 @@ def collate_locations(image_loc, image_mask):
     loc = np.array(np.concatenate([np.expand_dims(gl, 1), image_loc], 1), dtype=np.float32)
     mask = np.concatenate([np.repeat(np.array([[1]]), B, axis=0), image_mask], 1)
     return loc, mask
+
+
+def collate_pair_item(feat, num_boxes, image_loc, image_mask):
+    """K3MDataLoader.post_process (dataset:265-292): global row = sum of the region rows / RAW
+    num_boxes (no zero guard), location prefix [0,0,1,1,1], mask prefix 1."""
+    cnt = np.expand_dims(np.asarray(num_boxes), 1)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        g = np.sum(feat, axis=1) / cnt
+    f = np.array(np.concatenate([np.expand_dims(g, 1), feat], 1), dtype=np.float32)
+    loc, mask = collate_locations(image_loc, image_mask)
+    return f, loc, mask

@@ -194,6 +194,8 @@ def structure_aggregator(P, c_init, seq_pv, index_p, index_v, ent_neg, val_neg, 
         att = torch.softmax(b, dim=0)
         c_final.append(c_init[i] + linear(P, "struc_w3", (att * t).sum(0)))
     c_final = torch.stack(c_final, 0)
+    if ent_neg is None:   # item alignment: no LPM (vilbert_k3m.py:3288-3291)
+        return c_final, None
     pos, neg = [], []
     for i in range(B):
         for j in range(len(props[i])):
@@ -213,9 +215,10 @@ def structure_aggregator(P, c_init, seq_pv, index_p, index_v, ent_neg, val_neg, 
     return c_final, loss
 
 
-def forward(P, cfg, batch, noise=None, ent_neg=None, val_neg=None):
-    """Full pretraining forward (vilbert_k3m.py:2673-2846).  Returns a dict of the 10-tuple items
-    and the summed training loss of train_concap_struc.py:531-533 (loss_img_weight = 1)."""
+def encode(P, cfg, batch, noise=None):
+    """Embeddings, the three co-attention pair encoders, the initial-interactive fusion, pooling
+    and c_initial (bert_tri + get_sequence_pooled_output_final, vilbert_k3m.py:2376-2411, :2673-2725;
+    identical in K3MForItemAlignment.item_embedding :3329-3371)."""
     ids, tmask_i, tt = batch["input_ids"], batch["input_mask"], batch["segment_ids"]
     pids, pmask_i, ptt = batch["input_ids_pv"], batch["input_mask_pv"], batch["segment_ids_pv"]
     feat, loc, imask_i = batch["image_feat"], batch["image_loc"], batch["image_mask"]
@@ -239,6 +242,16 @@ def forward(P, cfg, batch, noise=None, ent_neg=None, val_neg=None):
     pooled_t = seq_t[:, 1:].mean(1)
     pooled_pv = seq_pv[:, 1:].mean(1)
     c_init = (pooled_v + pooled_t + pooled_pv) / 3
+    return dict(seq_v=seq_v, seq_t=seq_t, seq_pv=seq_pv, pooled_v=pooled_v, pooled_t=pooled_t, pooled_pv=pooled_pv,
+                c_init=c_init)
+
+
+def forward(P, cfg, batch, noise=None, ent_neg=None, val_neg=None):
+    """Full pretraining forward (vilbert_k3m.py:2673-2846).  Returns a dict of the 10-tuple items
+    and the summed training loss of train_concap_struc.py:531-533 (loss_img_weight = 1)."""
+    enc = encode(P, cfg, batch, noise)
+    seq_v, seq_t, seq_pv = enc["seq_v"], enc["seq_t"], enc["seq_pv"]
+    pooled_v, pooled_t, pooled_pv, c_init = enc["pooled_v"], enc["pooled_t"], enc["pooled_pv"], enc["c_init"]
     c_final, loss_lpm = structure_aggregator(P, c_init, seq_pv, batch["index_p"], batch["index_v"],
                                              ent_neg, val_neg, float(getattr(cfg, "margin", 1.0)))
 
@@ -271,6 +284,58 @@ def forward(P, cfg, batch, noise=None, ent_neg=None, val_neg=None):
                 next_sentence_loss=loss_nsp, loss_lpm=loss_lpm, c_initial=c_init, c_final=c_final,
                 pooled_t=pooled_t, pooled_pv=pooled_pv, pooled_v=pooled_v,
                 logits_t=lt, logits_pv=lpv, logits_v=lv)
+
+
+# ---------------------------------------------------------------- item alignment (fine-tuning)
+
+PAIR_KEYS = [("input_ids", "input_ids"), ("token_type_ids", "segment_ids"), ("attention_mask", "input_mask"),
+             ("input_ids_pv", "input_ids_pv"), ("token_type_ids_pv", "segment_ids_pv"),
+             ("attention_mask_pv", "input_mask_pv"), ("index_p", "index_p"), ("index_v", "index_v"),
+             ("image_feat", "image_feat"), ("image_loc", "image_loc"), ("image_attention_mask", "image_mask")]
+
+
+def item_batch(pair, k):
+    """The engine-named batch of item k (1 or 2) of a pair batch named as the arguments of
+    K3MForItemAlignment.forward (vilbert_k3m.py:3379-3403)."""
+    return {dst: pair["%s_%d" % (src, k)] for src, dst in PAIR_KEYS}
+
+
+def item_alignment_forward(P, cfg, pair, noise1=None, noise2=None):
+    """K3MForItemAlignment.forward (vilbert_k3m.py:3379-3456), eval mode.  Returns
+    (item_embedding_1, item_embedding_2, probs, loss) with the reference's quirks: for "ce" the
+    first two outputs are probs[:, 0] / probs[:, 1]; for "cosine" probs compares item 1 with itself
+    (:3443); "inner" has no loss function in the reference (AttributeError) and is rejected."""
+    es = []
+    for k, nz in ((1, noise1), (2, noise2)):
+        b = item_batch(pair, k)
+        enc = encode(P, cfg, b, nz)
+        c_final, _ = structure_aggregator(P, enc["c_init"], enc["seq_pv"], b["index_p"], b["index_v"], None, None, 0.0)
+        es.append(c_final)
+    e1, e2 = es
+    labels = pair["labels"]
+    lt = getattr(cfg, "loss_type", "ce")
+    if lt == "ce":
+        h = torch.tanh(linear(P, "classifier.dense", torch.cat((e1, e2), 1)))
+        logits = linear(P, "classifier.out_proj", h)
+        probs = torch.softmax(logits, dim=1)
+        loss = F.cross_entropy(logits.view(-1, 2), labels.view(-1).to(torch.long))
+        return probs[:, 0], probs[:, 1], probs[:, 1], loss
+    if lt == "cosine":
+        loss = F.cosine_embedding_loss(e1, e2, 2 * labels - 1, margin=0.0)
+        probs = (F.cosine_similarity(e1, e1) + 1) / 2
+        return e1, e2, probs, loss
+    raise ValueError("loss_type %r has no loss function in the reference" % lt)
+
+
+def adamw_torch_step(p, g, m, v, step, lr, wd, beta1=0.9, beta2=0.98, eps=1e-8):
+    """torch.optim.AdamW single-tensor math (finetune.py:356-361): decay first, bias-corrected denom."""
+    p.mul_(1.0 - lr * wd)
+    m.lerp_(g, 1.0 - beta1)
+    v.mul_(beta2).addcmul_(g, g, value=1.0 - beta2)
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+    p.addcdiv_(m, denom, value=-lr / bc1)
 
 
 # ---------------------------------------------------------------- optimizer

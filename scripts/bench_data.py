@@ -86,11 +86,11 @@ def main():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     with torch.cuda.stream(st):
         for _ in range(10):
-            _lib.call("k3m_collate_regions", feat.data_ptr(), R * F, zero.data_ptr(), mlab.data_ptr(), B, R, F,
+            _lib.call("k3m_collate_regions", feat.data_ptr(), R * F, zero.data_ptr(), mlab.data_ptr(), None, B, R, F,
                       out.data_ptr(), st.cuda_stream)
         e0.record(st)
         for _ in range(a.reps):
-            _lib.call("k3m_collate_regions", feat.data_ptr(), R * F, zero.data_ptr(), mlab.data_ptr(), B, R, F,
+            _lib.call("k3m_collate_regions", feat.data_ptr(), R * F, zero.data_ptr(), mlab.data_ptr(), None, B, R, F,
                       out.data_ptr(), st.cuda_stream)
         e1.record(st)
     torch.cuda.synchronize()

@@ -39,6 +39,7 @@ for s in "$@"; do
          step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python scripts/gemm_bench.py "fwd ffn1 gelu" 5
          step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python scripts/gemm_bench.py "fwd ffn1 gelu" 5 ;;
     data) step data 400 python -u -m pytest tests/test_gpu_data.py -x -v --timeout 120 --timeout-method thread ;;
+    ft) step ft 600 python -u -m pytest tests/test_gpu_finetune.py -x -v --timeout 300 --timeout-method thread ;;
     bdata) step bdata 300 python scripts/bench_data.py ;;
     pdata) export TMPDIR=/tmp; step pdata 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pdata -o run -- python scripts/bench_data.py --reps 50 ;;
     pmcdata) export TMPDIR=/tmp

@@ -33,3 +33,46 @@ def case_noise(g):
     rng = np.random.default_rng(int(g["noise_seed"]))
     shapes = [("v", (B, R, 3, 1024)), ("t", (B, T, 3, 768)), ("pv", (B, P, 3, 768))]
     return {k: torch.from_numpy((-np.log(rng.standard_exponential(s))).astype(np.float32)) for k, s in shapes}
+
+
+# ---------------------------------------------------------------- item alignment (fine-tuning)
+FT_CASES = ["ce", "cosine"]
+
+
+def load_ft_case(name):
+    d = np.load(os.path.join(HERE, "golden", "golden_ft_%s.npz" % name), allow_pickle=False)
+    return {k: d[k] for k in d.files}
+
+
+def ft_config(g):
+    from k3m_amd.config import finetune_config
+    return finetune_config(CFG_PATH, loss_type=str(g["loss_type"]), if_pre_sampling=int(g["mode"]))
+
+
+def ft_pair(g):
+    """Pair batch named as K3MForItemAlignment.forward's arguments (vilbert_k3m.py:3379-3403)."""
+    t = lambda k: torch.from_numpy(np.ascontiguousarray(g["out/" + k]))  # noqa: E731
+    pair = {"labels": t("labels")}
+    for k in (1, 2):
+        pair.update({"input_ids_%d" % k: t("input_ids_%d" % k), "token_type_ids_%d" % k: t("segment_ids_%d" % k),
+                     "attention_mask_%d" % k: t("input_mask_%d" % k), "input_ids_pv_%d" % k: t("input_ids_pv_%d" % k),
+                     "token_type_ids_pv_%d" % k: t("segment_ids_pv_%d" % k),
+                     "attention_mask_pv_%d" % k: t("input_mask_pv_%d" % k), "index_p_%d" % k: t("index_p_%d" % k),
+                     "index_v_%d" % k: t("index_v_%d" % k), "image_feat_%d" % k: t("coll_image_feat_%d" % k),
+                     "image_loc_%d" % k: t("coll_image_loc_%d" % k),
+                     "image_attention_mask_%d" % k: t("coll_image_mask_%d" % k)})
+    return pair
+
+
+def ft_noise(g):
+    """Gumbel noise per item (make_finetune_golden.py: noise_seed for item 1, noise_seed + 1 for item 2)."""
+    pair = ft_pair(g)
+    B, T = pair["input_ids_1"].shape
+    P = pair["input_ids_pv_1"].shape[1]
+    R = pair["image_feat_1"].shape[1]
+    out = []
+    for s in (int(g["noise_seed"]), int(g["noise_seed"]) + 1):
+        rng = np.random.default_rng(s)
+        shapes = [("v", (B, R, 3, 1024)), ("t", (B, T, 3, 768)), ("pv", (B, P, 3, 768))]
+        out.append({k: torch.from_numpy((-np.log(rng.standard_exponential(sh))).astype(np.float32)) for k, sh in shapes})
+    return out

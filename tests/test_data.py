@@ -124,3 +124,53 @@ def test_prepare_rejects_bad_records():
 D_FIELDS = ["item_id", "input_ids", "input_mask", "segment_ids", "lm_label_ids", "is_next", "input_ids_pv",
             "input_mask_pv", "segment_ids_pv", "lm_label_ids_pv", "is_next_pv_v", "is_next_pv_t", "index_p", "index_v",
             "image_feat", "image_loc", "image_target", "image_label", "image_mask", "masked_label"]
+
+
+# ---------------------------------------------------------------- fine-tuning pairs
+@pytest.fixture(scope="module")
+def ft_gold():
+    z = np.load(os.path.join(HERE, "golden", "golden_ft_data.npz"))
+    return {k: z[k] for k in z.files}
+
+
+def ft_records(g):
+    recs = []
+    for b in range(len(g["in/label"])):
+        rec = [int(g["in/label"][b])]
+        for k in (1, 2):
+            nb = int(g["in/num_boxes_%d" % k][b])
+            h, w = g["in/image_hw_%d" % k][b]
+            rec += [str(g["in/item_id_%d" % k][b]), str(g["in/caption_%d" % k][b]), str(g["in/pv_%d" % k][b]), "", h, w,
+                    nb, g["in/boxes_%d" % k][b, :nb], g["in/feat_%d" % k][b, :nb], g["in/target_%d" % k][b, :nb]]
+        recs.append(tuple(rec))
+    return recs
+
+
+def ft_preprocessor(g):
+    return D.K3MPreprocessBatch(char_tokenizer(), max_seq_len=int(g["cfg/max_seq_len"]),
+                                max_seq_len_pv=int(g["cfg/max_seq_len_pv"]), max_num_pv=int(g["cfg/max_num_pv"]),
+                                max_region_len=int(g["cfg/max_region_len"]), v_feature_size=int(g["cfg/v_feature_size"]),
+                                v_target_size=int(g["cfg/v_target_size"]))
+
+
+def test_finetune_preprocess_matches_reference(ft_gold):
+    g = ft_gold
+    pre = ft_preprocessor(g)
+    outs = [pre(r) for r in ft_records(g)]
+    for j, field in enumerate(D.PAIR_TUPLE):
+        if field.startswith("item_id"):
+            assert [o[j] for o in outs] == [str(x) for x in g["in/" + field]]
+            continue
+        got = np.stack([np.asarray(o[j]) for o in outs])
+        want = g["out/" + field]
+        assert got.shape == want.shape and np.array_equal(got, want), field
+    assert (g["in/num_boxes_1"] == 0).any() or (g["in/num_boxes_2"] == 0).any()
+
+
+def test_finetune_collation_restatement_matches_reference(ft_gold):
+    g = ft_gold
+    for k in (1, 2):
+        f, l, m = DO.collate_pair_item(g["out/image_feat_%d" % k], g["out/num_boxes_%d" % k], g["out/image_loc_%d" % k],
+                                       g["out/image_mask_%d" % k])
+        assert np.array_equal(f, g["out/coll_image_feat_%d" % k], equal_nan=True)
+        assert np.array_equal(l, g["out/coll_image_loc_%d" % k]) and np.array_equal(m, g["out/coll_image_mask_%d" % k])

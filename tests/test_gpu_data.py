@@ -54,7 +54,7 @@ def test_collate_kernel_full_size(B, R, F, p_zero, p_mask):
     fd = torch.from_numpy(feat).cuda()
     out = torch.full((B, R + 1, F), float("nan"), device="cuda")
     zd, md = torch.from_numpy(zero).cuda(), torch.from_numpy(mlab).cuda()   # kept alive across the launch
-    _lib.call("k3m_collate_regions", fd.data_ptr(), R * F, zd.data_ptr(), md.data_ptr(), B, R, F, out.data_ptr(),
+    _lib.call("k3m_collate_regions", fd.data_ptr(), R * F, zd.data_ptr(), md.data_ptr(), None, B, R, F, out.data_ptr(),
               _lib.stream())
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), want)
