@@ -229,6 +229,19 @@ int k3m_sa_gather_bwd(const float* dX, const int64_t* index_p, const int64_t* in
 int k3m_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, long long n, double lr, double beta1,
               double beta2, double eps, double wd, int step, float grad_scale, hipStream_t stream);
 
+/* Attention for sequences longer than 128 (up to 512 keys, d <= 128): the fine-tuning PV text
+ * (max_seq_length_pv 256, finetune.py:1275) and SURVEY config 5 (P = 320).  Same arguments,
+ * semantics, probability layout and dropout counters as k3m_attn_fwd / k3m_attn_bwd; the backward
+ * takes a workspace ds_ws of the probabilities' size (fp32 [nseq*nh*lq*lk]). */
+int k3m_attn_long_fwd(const void* q, long long ldq, const void* k, long long ldk, const void* v, long long ldv,
+                      const float* kmask, void* ctx, long long ldc, float* probs, int nseq, int lq, int lk, int nh,
+                      int hd, float scale, float p_drop, uint64_t seed, uint64_t off, int dtype, hipStream_t stream);
+int k3m_attn_long_bwd(const void* dctx, long long ldc, const void* o, long long ldo, const void* q, long long ldq,
+                      const void* k, long long ldk, const void* v, long long ldv, const float* probs, float* ds_ws,
+                      void* dq, void* dk, void* dv, long long lddq, long long lddk, long long lddv, int nseq, int lq,
+                      int lk, int nh, int hd, float scale, float p_drop, uint64_t seed, uint64_t off, int dtype,
+                      hipStream_t stream);
+
 /* torch.optim.AdamW (decoupled decay applied first, eps added after the bias correction of sqrt(v)):
  * the optimizer of the fine-tuning driver (finetune.py:356-361).  Same arguments as k3m_adamw. */
 int k3m_adamw_torch(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, long long n, double lr,

@@ -7,7 +7,7 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libk3m_hip.so")
-SOURCES = ["gemm.hip", "gemm_bf16.hip", "norm.hip", "attention.hip", "attention_bf16.hip", "loss.hip", "fusion.hip", "struct.hip", "adamw.hip", "data.hip", "align.hip"]
+SOURCES = ["gemm.hip", "gemm_bf16.hip", "norm.hip", "attention.hip", "attention_bf16.hip", "loss.hip", "fusion.hip", "struct.hip", "adamw.hip", "data.hip", "align.hip", "attention_long.hip"]
 FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-mcode-object-version=5", "-Wno-unused-result"]
 
 

@@ -20,7 +20,13 @@
 #pragma once
 #include "common.h"
 
-namespace k3m_f32 {
+// The lab (scripts/lab) compiles these templates into its own executable under other namespace
+// names: kernels with the same mangled name as libk3m_hip.so's would resolve to the library's code.
+#ifndef K3M_F32_NS
+#define K3M_F32_NS k3m_f32
+#endif
+
+namespace K3M_F32_NS {
 
 constexpr int BK = 32;
 
@@ -191,9 +197,9 @@ __device__ __forceinline__ void mainloop(const float* __restrict__ A, long long 
   }
 }
 
-}  // namespace k3m_f32
+}  // namespace K3M_F32_NS
 
-namespace k3m_f32 {
+namespace K3M_F32_NS {
 
 // Epilogue, staged through LDS (free after the main loop's last barrier) so that global traffic is
 // row-contiguous 16-B vectors: each wave writes one 32-row slice of its accumulators into a private
@@ -327,4 +333,4 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_f32_kernel(K3mGemm g) 
   epilogue<TBM, TBN, WM, WN, EPI>(g, m0, n0, smem, acc);
 }
 
-}  // namespace k3m_f32
+}  // namespace K3M_F32_NS

@@ -21,7 +21,11 @@
 #pragma once
 #include "gemm_f32_tile.h"
 
-namespace k3m_x6 {
+#ifndef K3M_X6_NS
+#define K3M_X6_NS k3m_x6
+#endif
+
+namespace K3M_X6_NS {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));
@@ -72,6 +76,12 @@ __device__ __forceinline__ bf16x8 mn_frag(const __bf16* img, int mn_base, int ks
 // exact three-way split of a float pair into packed bf16 planes h, m, l (a = h + m + l exactly):
 // per pair 3 conversions, 2 x (unpack lo/hi + subtract) = ~4.5 VALU per element
 __device__ __forceinline__ void split2(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
+#ifdef K3M_X6_LAB_NO_SPLIT   // lab only (scripts/lab): the cost of the main loop without the split VALU
+  h = pk_bf16(a, b);
+  m = h;
+  l = h;
+  return;
+#endif
   h = pk_bf16(a, b);
   const float r1a = a - __uint_as_float(h << 16), r1b = b - __uint_as_float(h & 0xffff0000u);
   m = pk_bf16(r1a, r1b);
@@ -210,7 +220,11 @@ __device__ __forceinline__ void store_tile(__bf16* __restrict__ lds, const Stage
   }
 }
 
-template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool VEC, bool PIPE = true>
+// VAR (tuning bits, lab-selectable): 1 = pin the next tile's global loads at the top of each step
+// (sched_barrier), 2 = static s_setprio 1 for the second half of the waves (MI355X_MICROARCH.md,
+// "Two waves per SIMD" item 4), 4 = pin the split+store after the MFMAs, 8 = s_setprio 1 for the
+// first half instead.
+template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool VEC, bool PIPE = true, int VAR = 0>
 __device__ __forceinline__ void mainloop(const float* __restrict__ A, long long lda, const float* __restrict__ B,
                                          long long ldb, int M, int N, int m0, int n0, int kbeg, int kend,
                                          __bf16* smem, floatx16 (&acc)[TBM / WM / 32][TBN / WN / 32]) {
@@ -268,6 +282,12 @@ __device__ __forceinline__ void mainloop(const float* __restrict__ A, long long 
         }
     }
   };
+  if constexpr ((VAR & 2) != 0) {
+    if (w >= WM * WN / 2) __builtin_amdgcn_s_setprio(1);
+  }
+  if constexpr ((VAR & 8) != 0) {
+    if (w < WM * WN / 2) __builtin_amdgcn_s_setprio(1);
+  }
   if constexpr (!PIPE) {
     // one register set: prefetch tile kt+1 while computing tile kt, write it after the MFMAs
     // (fewer VGPRs: lets two 8-wave blocks share a CU)
@@ -315,7 +335,9 @@ __device__ __forceinline__ void mainloop(const float* __restrict__ A, long long 
       // even step: compute stage 0 | split ra1/rb1 (tile kt+1) -> stage 1 | load tile kt+2 -> ra/rb
       load_full<AK, TBM, BK, NT>(sa, lda, ra, kt + 3 < nkf);
       load_full<BK_, TBN, BK, NT>(sb, ldb, rb, kt + 3 < nkf);
+      if constexpr ((VAR & 1) != 0) __builtin_amdgcn_sched_barrier(0);
       compute(0);
+      if constexpr ((VAR & 4) != 0) __builtin_amdgcn_sched_barrier(0);
       store_tile<AK, TBM, BK, NT>(smem + BUF, ra1);
       store_tile<BK_, TBN, BK, NT>(smem + BUF + 3 * PA, rb1);
       __syncthreads();
@@ -323,12 +345,16 @@ __device__ __forceinline__ void mainloop(const float* __restrict__ A, long long 
       // odd step: compute stage 1 | split ra/rb (tile kt+2) -> stage 0 | load tile kt+3 -> ra1/rb1
       load_full<AK, TBM, BK, NT>(sa, lda, ra1, kt + 4 < nkf);
       load_full<BK_, TBN, BK, NT>(sb, ldb, rb1, kt + 4 < nkf);
+      if constexpr ((VAR & 1) != 0) __builtin_amdgcn_sched_barrier(0);
       compute(1);
+      if constexpr ((VAR & 4) != 0) __builtin_amdgcn_sched_barrier(0);
       store_tile<AK, TBM, BK, NT>(smem, ra);
       store_tile<BK_, TBN, BK, NT>(smem + 3 * PA, rb);
       __syncthreads();
     }
+
   }
+  if constexpr ((VAR & 10) != 0) __builtin_amdgcn_s_setprio(0);
   if (krem > 0) {  // peeled partial k-tile (masked loads); the pointers rest on the last full tile
     const int cur = nkf & 1;
     if (nkf > 0) {
@@ -345,14 +371,15 @@ __device__ __forceinline__ void mainloop(const float* __restrict__ A, long long 
   }
 }
 
-template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool VEC, int EPI, int OCC, bool PIPE = true>
+template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool VEC, int EPI, int OCC, bool PIPE = true,
+          int VAR = 0>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_x6_kernel(K3mGemm g) {
   constexpr int LDS_BF16 = 2 * 3 * (TBM + TBN) * BK;
   constexpr int EPI_F32 = WM * WN * 32 * (TBN / WN + 8);
   constexpr int WORDS = (LDS_BF16 / 2 > EPI_F32 ? LDS_BF16 / 2 : EPI_F32);
   __shared__ __attribute__((aligned(16))) float smem[WORDS];
   int m0, n0;
-  k3m_f32::tile_coords(g.m, g.n, TBM, TBN, m0, n0);
+  K3M_F32_NS::tile_coords(g.m, g.n, TBM, TBN, m0, n0);
   int kbeg = 0, kend = g.k;
   if (g.splitk > 1) {
     const int per = ((g.k + g.splitk - 1) / g.splitk + BK - 1) / BK * BK;
@@ -360,9 +387,9 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_x6_kernel(K3mGemm g) {
     kend = min(g.k, kbeg + per);
   }
   floatx16 acc[TBM / WM / 32][TBN / WN / 32];
-  mainloop<TBM, TBN, WM, WN, BK, AK, BK_, VEC, PIPE>(static_cast<const float*>(g.a), g.lda, static_cast<const float*>(g.b),
+  mainloop<TBM, TBN, WM, WN, BK, AK, BK_, VEC, PIPE, VAR>(static_cast<const float*>(g.a), g.lda, static_cast<const float*>(g.b),
                                                g.ldb, g.m, g.n, m0, n0, kbeg, kend, reinterpret_cast<__bf16*>(smem), acc);
-  k3m_f32::epilogue<TBM, TBN, WM, WN, EPI, WORDS>(g, m0, n0, smem, acc);
+  K3M_F32_NS::epilogue<TBM, TBN, WM, WN, EPI, WORDS>(g, m0, n0, smem, acc);
 }
 
-}  // namespace k3m_x6
+}  // namespace K3M_X6_NS

@@ -196,16 +196,17 @@ class FFN(object):
         return dh
 
 
-def _flash(q, hd):
-    # bf16 encoder: the LSE-saving bf16 kernels (attention_bf16.hip); fp32: exact-fp32 kernels
-    return q.dtype == torch.bfloat16 and hd in (64, 96, 128)
+def _flash(q, hd, lq, lk):
+    # bf16 encoder: the LSE-saving bf16 kernels (attention_bf16.hip, L <= 128); fp32 and longer
+    # sequences: the exact-fp32 kernels (attention.hip, attention_long.hip)
+    return q.dtype == torch.bfloat16 and hd in (64, 96, 128) and max(lq, lk) <= ops.SHORT_MAXL
 
 
 def _attn_fwd(q, k, v, mask, nseq, lq, lk, nh, p, rng, out=None):
     hd = q.shape[1] // nh
     ctx = out if out is not None else torch.empty((nseq * lq, q.shape[1]), dtype=q.dtype, device=q.device)
     off = rng.take(nseq * nh * lq * lk) if p > 0 else 0
-    if _flash(q, hd):
+    if _flash(q, hd, lq, lk):
         stat = torch.empty((nseq * nh * lq,), dtype=torch.float32, device=q.device)   # row LSE
         ops.flash_attn_fwd(q, k, v, mask, ctx, stat, nseq, lq, lk, nh, hd, 1.0 / math.sqrt(hd), p, rng.seed, off)
     else:
@@ -216,7 +217,7 @@ def _attn_fwd(q, k, v, mask, nseq, lq, lk, nh, p, rng, out=None):
 
 def _attn_bwd(dctx, o, q, k, v, saved, dq, dk, dv):
     stat, mask, nseq, lq, lk, nh, hd, p, seed, off = saved
-    if _flash(q, hd):
+    if _flash(q, hd, lq, lk):
         ops.flash_attn_bwd(dctx, o, q, k, v, mask, stat, dq, dk, dv, nseq, lq, lk, nh, hd, 1.0 / math.sqrt(hd), p,
                            seed, off)
     else:

@@ -152,15 +152,25 @@ def embed_bwd(ids, tt, ds, dword, dpos, dtyp):
 
 
 # ------------------------------------------------------------------ attention
+SHORT_MAXL = 128   # attention.hip keeps a whole head in LDS up to this length; attention_long.hip beyond
+
+
 def attn_fwd(q, k, v, kmask, ctx, probs, nseq, lq, lk, nh, hd, scale, p_drop, seed, off):
-    call("k3m_attn_fwd", ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v), ptr(kmask), ptr(ctx), _ld(ctx), ptr(probs),
+    name = "k3m_attn_fwd" if max(lq, lk) <= SHORT_MAXL else "k3m_attn_long_fwd"
+    call(name, ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v), ptr(kmask), ptr(ctx), _ld(ctx), ptr(probs),
          nseq, lq, lk, nh, hd, scale, p_drop, seed, off, dt(ctx), stream())
 
 
 def attn_bwd(dctx, o, q, k, v, probs, dq, dk, dv, nseq, lq, lk, nh, hd, scale, p_drop, seed, off):
-    call("k3m_attn_bwd", ptr(dctx), _ld(dctx), ptr(o), _ld(o), ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v), ptr(probs), ptr(dq),
-         ptr(dk), ptr(dv), _ld(dq), _ld(dk), _ld(dv), nseq, lq, lk, nh, hd, scale, p_drop, seed, off, dt(dctx),
-         stream())
+    if max(lq, lk) <= SHORT_MAXL:
+        call("k3m_attn_bwd", ptr(dctx), _ld(dctx), ptr(o), _ld(o), ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v),
+             ptr(probs), ptr(dq), ptr(dk), ptr(dv), _ld(dq), _ld(dk), _ld(dv), nseq, lq, lk, nh, hd, scale, p_drop,
+             seed, off, dt(dctx), stream())
+        return
+    ws = torch.empty_like(probs)
+    call("k3m_attn_long_bwd", ptr(dctx), _ld(dctx), ptr(o), _ld(o), ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v),
+         ptr(probs), ptr(ws), ptr(dq), ptr(dk), ptr(dv), _ld(dq), _ld(dk), _ld(dv), nseq, lq, lk, nh, hd, scale,
+         p_drop, seed, off, dt(dctx), stream())
 
 
 def flash_attn_fwd(q, k, v, kmask, ctx, lse, nseq, lq, lk, nh, hd, scale, p_drop, seed, off):

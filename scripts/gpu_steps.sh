@@ -40,6 +40,8 @@ for s in "$@"; do
          step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python scripts/gemm_bench.py "fwd ffn1 gelu" 5 ;;
     data) step data 400 python -u -m pytest tests/test_gpu_data.py -x -v --timeout 120 --timeout-method thread ;;
     ft) step ft 600 python -u -m pytest tests/test_gpu_finetune.py -x -v --timeout 300 --timeout-method thread ;;
+    bft) step bft 600 python scripts/bench_finetune.py --steps 10 --warmup 3 ;;
+    pft) export TMPDIR=/tmp; step pft 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pft -o run -- python scripts/bench_finetune.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     bdata) step bdata 300 python scripts/bench_data.py ;;
     pdata) export TMPDIR=/tmp; step pdata 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pdata -o run -- python scripts/bench_data.py --reps 50 ;;
     pmcdata) export TMPDIR=/tmp

@@ -2,6 +2,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
+#define K3M_F32_NS lab_f32
+#define K3M_X6_NS lab_x6
 #include "../../k3m_amd/csrc/gemm_x6_tile.h"
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
@@ -25,19 +27,19 @@ __global__ void count_bad(const float* c, const double* r, long long n, double t
 template <int TBM, int TBN, int WM, int WN, int BK, int OCC, int EPI>
 void launch(const K3mGemm& g, hipStream_t st) {
   const int tm = (g.m + TBM - 1) / TBM, tn = (g.n + TBN - 1) / TBN;
-  hipLaunchKernelGGL((k3m_x6::gemm_x6_kernel<TBM, TBN, WM, WN, BK, true, false, true, EPI, OCC>), dim3(tm * tn), dim3(64 * WM * WN), 0, st, g);
+  hipLaunchKernelGGL((lab_x6::gemm_x6_kernel<TBM, TBN, WM, WN, BK, true, false, true, EPI, OCC>), dim3(tm * tn), dim3(64 * WM * WN), 0, st, g);
 }
 
 __global__ void visit_kernel(int M, int N, int TBM, int TBN, int* visits) {
   int m0, n0;
-  k3m_f32::tile_coords(M, N, TBM, TBN, m0, n0);
+  lab_f32::tile_coords(M, N, TBM, TBN, m0, n0);
   if (threadIdx.x == 0) atomicAdd(&visits[(m0 / TBM) * ((N + TBN - 1) / TBN) + n0 / TBN], 1);
 }
 
 template <int TBM, int TBN, int WM, int WN, int OCC, int EPI>
 void launch_f32(const K3mGemm& g, hipStream_t st) {
   const int tm = (g.m + TBM - 1) / TBM, tn = (g.n + TBN - 1) / TBN;
-  hipLaunchKernelGGL((k3m_f32::gemm_f32_kernel<TBM, TBN, WM, WN, true, false, true, EPI, OCC>), dim3(tm * tn), dim3(64 * WM * WN), 0, st, g);
+  hipLaunchKernelGGL((lab_f32::gemm_f32_kernel<TBM, TBN, WM, WN, true, false, true, EPI, OCC>), dim3(tm * tn), dim3(64 * WM * WN), 0, st, g);
 }
 
 int main() {

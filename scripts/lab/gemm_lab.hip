@@ -6,6 +6,8 @@
 #include <vector>
 #include <string>
 #include <cstring>
+#define K3M_F32_NS lab_f32
+#define K3M_X6_NS lab_x6
 #include "../../k3m_amd/csrc/gemm_x6_tile.h"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
@@ -33,7 +35,7 @@ __global__ void maxdiff_kernel(const float* a, const float* b, long long n, floa
   if ((threadIdx.x & 63) == 0) { atomicMax((int*)out, __float_as_int(m)); atomicMax((int*)out + 1, __float_as_int(r)); }
 }
 
-using namespace k3m_f32;
+using namespace lab_f32;
 
 typedef void (*Launcher)(const K3mGemm&, hipStream_t);
 
@@ -44,11 +46,11 @@ void launch(const K3mGemm& g, hipStream_t st) {
   hipLaunchKernelGGL((gemm_f32_kernel<TBM, TBN, WM, WN, AK, BK_, true, EPI, OCC>), grid, dim3(64 * WM * WN), 0, st, g);
 }
 
-template <int TBM, int TBN, int WM, int WN, int BK, int OCC, int EPI, bool AK, bool BK_, bool PIPE = true>
+template <int TBM, int TBN, int WM, int WN, int BK, int OCC, int EPI, bool AK, bool BK_, bool PIPE = true, int VAR = 0>
 void launch_x6(const K3mGemm& g, hipStream_t st) {
   const int tm = (g.m + TBM - 1) / TBM, tn = (g.n + TBN - 1) / TBN;
   dim3 grid(tm * tn, g.splitk > 1 ? g.splitk : 1);
-  hipLaunchKernelGGL((k3m_x6::gemm_x6_kernel<TBM, TBN, WM, WN, BK, AK, BK_, true, EPI, OCC, PIPE>), grid, dim3(64 * WM * WN), 0, st, g);
+  hipLaunchKernelGGL((lab_x6::gemm_x6_kernel<TBM, TBN, WM, WN, BK, AK, BK_, true, EPI, OCC, PIPE, VAR>), grid, dim3(64 * WM * WN), 0, st, g);
 }
 
 // fp64 reference C = A.B^T (nt) for the accuracy check
@@ -72,15 +74,23 @@ __global__ void err_kernel(const float* c, const double* r, long long n, double*
 
 struct Shape { const char* name; int kind; int m, n, k, epi, splitk; };  // kind 0 nt, 1 nn, 2 tn
 
+void launch_shipped(const K3mGemm& g, hipStream_t st) { k3m_gemm(&g, st); }
+
 template <int EPI, bool AK, bool BK_>
 std::vector<std::pair<std::string, Launcher>> variants() {
   return {
-      {"x6 256x256 2x4 bk16", launch_x6<256, 256, 2, 4, 16, 1, EPI, AK, BK_>},
+      {"shipped in loop", launch_shipped},
       {"x6 256x128 4x2 bk32", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_>},
-      {"x6 256x128 bk16 2blk nopipe", launch_x6<256, 128, 4, 2, 16, 4, EPI, AK, BK_, false>},
+      {"x6 256x128 bk32 v2 prio", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, true, 2>},
+      {"x6 256x128 bk32 v3 loadpin+prio", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, true, 3>},
+      {"x6 256x128 bk32 v6 prio+storepin", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, true, 6>},
+      {"x6 256x128 bk32 v7 all", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, true, 7>},
+      {"x6 256x128 bk32 v8 prio-first", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, true, 8>},
+      {"x6 256x128 bk32 v12 prio-first+storepin", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, true, 12>},
+      {"x6 256x128 bk32 nopipe v2", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, false, 2>},
+      {"x6 256x128 bk32 nopipe v8", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, false, 8>},
+      {"x6 256x128 bk16 2blk nopipe v8", launch_x6<256, 128, 4, 2, 16, 4, EPI, AK, BK_, false, 8>},
       {"x6 256x128 bk32 nopipe", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, false>},
-      {"x6 128x128 bk32 o1", launch_x6<128, 128, 2, 2, 32, 1, EPI, AK, BK_>},
-      {"x6 128x128 bk16 3blk nopipe", launch_x6<128, 128, 2, 2, 16, 3, EPI, AK, BK_, false>},
   };
 }
 
@@ -185,6 +195,8 @@ int main(int argc, char** argv) {
     run_ref();
     std::vector<std::pair<std::string, Launcher>> vs =
         s.kind == 0 ? variants_epi<true, true>(s.epi) : s.kind == 1 ? variants_epi<true, false>(s.epi) : variants_epi<false, false>(s.epi);
+    const int passes = getenv("LAB_PASSES") ? atoi(getenv("LAB_PASSES")) : 1;
+    for (int pass = 0; pass < passes; ++pass)
     for (auto& v : vs) {
       if (only_var && !strstr(v.first.c_str(), only_var)) continue;
       K3mGemm gv = g;
