@@ -33,8 +33,8 @@ REF_FLOPS_PER_SAMPLE = 319.31e9   # reference algorithmic fwd+bwd FLOPs/sample a
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
                     help="fp32: configs[1] (the metric's config); bf16: mixed-precision encoder (configs[2])")

@@ -67,6 +67,11 @@ typedef struct K3mGemm {
   int f32_algo;          /* fp32 operands: K3M_F32_SPLIT_BF16X6 (0, default) or K3M_F32_MFMA_F32 */
 } K3mGemm;
 int k3m_gemm(const K3mGemm* g, hipStream_t stream);
+/* Up to 8 INDEPENDENT problems in one launch (no problem may read another's output).  When all share
+ * one kernel template (fp32 operands on the bf16x6 path, same a_trans / b_trans / epilogue, 16-B
+ * aligned) they run as one grid of 256x128 tiles — the co-attention blocks' six small GEMMs per
+ * step of the wide engine; otherwise each runs through k3m_gemm. */
+int k3m_gemm_grouped(const K3mGemm* gs, int count, hipStream_t stream);
 
 /* out[c] (+)= sum_r x[r*ld + c]  — bias gradients (autograd of every Linear bias).
  * ws: >= (256 + 16)*cols floats. */

@@ -69,6 +69,7 @@ SIGNATURES = {
     "k3m_cast_f32_bf16": [vp, vp, i64, vp],
     "k3m_convert": [vp, i32, vp, i32, i64, i32, f32, vp],
     "k3m_add_inplace": [vp, vp, i64, f32, i32, vp],
+    "k3m_gemm_grouped": [vp, i32, vp],
     "k3m_collate_regions": [vp, i64, vp, vp, vp, i32, i32, i32, vp, vp],
     "k3m_attn_long_fwd": [vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, i32, f32, f32, u64, u64, i32,
                           vp],

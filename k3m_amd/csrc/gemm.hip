@@ -101,7 +101,7 @@ int launch_x6(const K3mGemm& g, bool ak, bool bk, hipStream_t st) {
   // both operands MN-contiguous (the weight gradients dY^T.X): the single-register-set loop measured
   // 5-7% faster than the two-set pipeline on these shapes (scripts/lab, best of passes)
   if constexpr (TBM == 256) return launch_x6_epi<TBM, TBN, WM, WN, BK, OCC, false, false, false>(g, st);
-  return launch_x6_epi<TBM, TBN, WM, WN, BK, OCC, false, false>(g, st);
+  else return launch_x6_epi<TBM, TBN, WM, WN, BK, OCC, false, false>(g, st);
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -154,6 +154,90 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, g.ws, g.splitk, g.m, g.n,
                        static_cast<float*>(g.c), g.ldc, g.alpha, g.beta);
     K3M_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------ grouped launch
+namespace {
+
+template <bool AK, bool BK_, bool PIPE>
+int launch_grouped_epi(const k3m_x6::GemmGroup& grp, int epi, hipStream_t st) {
+  const dim3 grid(grp.start[grp.count]);
+  switch (epi) {
+#define K3M_GROUP_CASE(E)                                                                                          \
+    case E:                                                                                                        \
+      hipLaunchKernelGGL((k3m_x6::gemm_x6_grouped_kernel<256, 128, 4, 2, 32, AK, BK_, true, E, 1, PIPE>), grid,       \
+                         dim3(512), 0, st, grp);                                                                   \
+      break;
+    K3M_GROUP_CASE(K3M_EPI_NONE)
+    K3M_GROUP_CASE(K3M_EPI_BIAS)
+    K3M_GROUP_CASE(K3M_EPI_BIAS_GELU)
+    K3M_GROUP_CASE(K3M_EPI_DGELU)
+    K3M_GROUP_CASE(K3M_EPI_BIAS_SIGMOID)
+#undef K3M_GROUP_CASE
+    default: return K3M_EINVAL;
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int k3m_gemm_grouped(const K3mGemm* gs, int count, hipStream_t st) {
+  K3M_ARG(gs && count >= 0 && count <= k3m_x6::GROUP_MAX);
+  if (count == 0) return 0;
+  // one template for the whole group: same layout, epilogue, dtype, algorithm, 16-B aligned operands
+  const K3mGemm& g0 = gs[0];
+  bool same = g0.dtype == K3M_F32 && g0.c_dtype == K3M_F32 && g0.f32_algo == K3M_F32_SPLIT_BF16X6;
+  k3m_x6::GemmGroup grp = {};
+  int nb = 0, live = 0;
+  for (int i = 0; i < count && same; ++i) {
+    const K3mGemm& g = gs[i];
+    same = g.a_trans == g0.a_trans && g.b_trans == g0.b_trans && g.epilogue == g0.epilogue && g.dtype == g0.dtype &&
+           g.c_dtype == g0.c_dtype && g.f32_algo == g0.f32_algo;
+    const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
+    same = same && aligned16(g.a) && (g.lda % 4 == 0) && ((ak ? g.k : g.m) % 4 == 0) && aligned16(g.b) &&
+           (g.ldb % 4 == 0) && ((bk ? g.k : g.n) % 4 == 0);
+    if (g.m == 0 || g.n == 0) continue;
+    grp.g[live] = g;
+    grp.start[live] = nb;
+    nb += (int)nblocks(g, 256, 128);
+    ++live;
+  }
+  if (!same) {   // not one template: launch each on its own
+    for (int i = 0; i < count; ++i) {
+      const int rc = k3m_gemm(&gs[i], st);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  for (int i = 0; i < live; ++i) {
+    const K3mGemm& g = grp.g[i];
+    K3M_ARG(g.a && g.b && g.c && g.k >= 0);
+    K3M_ARG(g.splitk <= 1 || (g.epilogue == K3M_EPI_NONE && g.ws));
+    K3M_ARG(g.epilogue == K3M_EPI_NONE || g.epilogue == K3M_EPI_DGELU || g.bias);
+    K3M_ARG((g.epilogue != K3M_EPI_BIAS_GELU && g.epilogue != K3M_EPI_DGELU) || g.aux);
+  }
+  if (live == 0) return 0;
+  grp.start[live] = nb;
+  grp.count = live;
+  const bool ak = g0.a_trans == 0, bk = g0.b_trans == 1;
+  int rc;
+  if (ak && bk) rc = launch_grouped_epi<true, true, true>(grp, g0.epilogue, st);
+  else if (ak) rc = launch_grouped_epi<true, false, true>(grp, g0.epilogue, st);
+  else if (bk) rc = launch_grouped_epi<false, true, true>(grp, g0.epilogue, st);
+  else rc = launch_grouped_epi<false, false, false>(grp, g0.epilogue, st);
+  if (rc) return rc;
+  K3M_CHECK_LAUNCH();
+  for (int i = 0; i < live; ++i) {
+    const K3mGemm& g = grp.g[i];
+    if (g.splitk > 1) {
+      const long long total = (long long)g.m * g.n;
+      const int blocks = (int)std::min<long long>((total + 255) / 256, 2048);
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, g.ws, g.splitk, g.m, g.n,
+                         static_cast<float*>(g.c), g.ldc, g.alpha, g.beta);
+      K3M_CHECK_LAUNCH();
+    }
   }
   return 0;
 }

@@ -210,7 +210,7 @@ namespace K3M_F32_NS {
 // by the reduction kernel).
 template <int TBM, int TBN, int WM, int WN, int EPI, int CAP = 2 * (TBM + TBN) * BK>
 __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, float* smem,
-                                         const floatx16 (&acc)[TBM / WM / 32][TBN / WN / 32]) {
+                                         const floatx16 (&acc)[TBM / WM / 32][TBN / WN / 32], int slice = -1) {
   constexpr int FM = TBM / WM / 32, FN = TBN / WN / 32;
   constexpr int WCOLS = FN * 32, WS = WCOLS + 8, LPR = WCOLS / 8, RPP = 64 / LPR;
   static_assert(WM * WN * 32 * WS <= CAP, "epilogue staging exceeds the LDS tile");
@@ -220,7 +220,7 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, float
   const int M = g.m, N = g.n;
   float* wl = smem + w * 32 * WS;
   const bool split = g.splitk > 1;
-  float* C = split ? g.ws + (long long)blockIdx.y * M * N : static_cast<float*>(g.c);
+  float* C = split ? g.ws + (long long)(slice >= 0 ? slice : (int)blockIdx.y) * M * N : static_cast<float*>(g.c);
   const long long ldc = split ? N : g.ldc;
   const float alpha = split ? 1.f : g.alpha, beta = split ? 0.f : g.beta;
   float* aux = static_cast<float*>(g.aux);

@@ -392,4 +392,43 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_x6_kernel(K3mGemm g) {
   K3M_F32_NS::epilogue<TBM, TBN, WM, WN, EPI, WORDS>(g, m0, n0, smem, acc);
 }
 
+// Grouped launch: several independent problems that share the kernel template (layout,
+// epilogue) in ONE grid — the co-attention blocks' GEMMs (three blocks x two streams, each only
+// 2,304-8,192 rows) fill the 256 CUs together where each alone leaves CUs idle or falls back to a
+// small tile.  blocks [start[p], start[p+1]) belong to problem p, split-major (slice, tile).
+constexpr int GROUP_MAX = 8;
+struct GemmGroup {
+  K3mGemm g[GROUP_MAX];
+  int start[GROUP_MAX + 1];
+  int count;
+};
+
+template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool VEC, int EPI, int OCC, bool PIPE = true>
+__global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_x6_grouped_kernel(GemmGroup grp) {
+  constexpr int LDS_BF16 = 2 * 3 * (TBM + TBN) * BK;
+  constexpr int EPI_F32 = WM * WN * 32 * (TBN / WN + 8);
+  constexpr int WORDS = (LDS_BF16 / 2 > EPI_F32 ? LDS_BF16 / 2 : EPI_F32);
+  __shared__ __attribute__((aligned(16))) float smem[WORDS];
+  const int id = K3M_F32_NS::xcd_remap(blockIdx.x, grp.start[grp.count]);
+  int p = 0;
+  while (p + 1 < grp.count && id >= grp.start[p + 1]) ++p;
+  const K3mGemm& g = grp.g[p];
+  const int tm = (g.m + TBM - 1) / TBM, tn = (g.n + TBN - 1) / TBN, tiles = tm * tn;
+  const int local = id - grp.start[p], slice = local / tiles, t = local - slice * tiles;
+  constexpr int GROUP = 8;   // tile order inside a problem: GROUP row-tiles walk N together
+  const int group_sz = GROUP * tn, first_m = (t / group_sz) * GROUP, gm_sz = min(tm - first_m, GROUP);
+  const int m0 = (first_m + (t % group_sz) % gm_sz) * TBM, n0 = ((t % group_sz) / gm_sz) * TBN;
+  int kbeg = 0, kend = g.k;
+  if (g.splitk > 1) {
+    const int per = ((g.k + g.splitk - 1) / g.splitk + BK - 1) / BK * BK;
+    kbeg = slice * per;
+    kend = min(g.k, kbeg + per);
+  }
+  floatx16 acc[TBM / WM / 32][TBN / WN / 32];
+  mainloop<TBM, TBN, WM, WN, BK, AK, BK_, VEC, PIPE>(static_cast<const float*>(g.a), g.lda,
+                                                     static_cast<const float*>(g.b), g.ldb, g.m, g.n, m0, n0, kbeg,
+                                                     kend, reinterpret_cast<__bf16*>(smem), acc);
+  K3M_F32_NS::epilogue<TBM, TBN, WM, WN, EPI, WORDS>(g, m0, n0, smem, acc, slice);
+}
+
 }  // namespace K3M_X6_NS

@@ -24,6 +24,7 @@ gradients are accumulated in place by the GEMM epilogue (beta = 1) and bias/LN g
 reduction kernels, so there is no autograd bookkeeping on the hot path.
 """
 import math
+import os
 
 import torch
 
@@ -320,6 +321,87 @@ class ConnectionOp(object):
         self.qkv2.dgrad(dq2, dx=ds2, beta=1.0)
 
 
+    # ---- lock-step form: the same computation as fwd / bwd cut into segments at the GEMM stages, so
+    # the three co-attention blocks of one schedule step issue their (independent) GEMMs together and
+    # each stage runs as one grouped launch (_lockstep).  Inside a segment no op reads a GEMM output
+    # of the same segment.
+    def fwd_steps(self, s1, s2, nseq, l1, l2, mask1, mask2, rng, out1, out2, res):
+        Hb = self.qkv1.W.shape[0] // 3
+        q1 = self.qkv1.fwd(s1)
+        q2 = self.qkv2.fwd(s2)
+        yield
+        ctx1, a1s = _attn_fwd(q2[:, 0:Hb], q1[:, Hb:2 * Hb], q1[:, 2 * Hb:], mask1, nseq, l2, l1, self.nh, self.pa1, rng)
+        ctx2, a2s = _attn_fwd(q1[:, 0:Hb], q2[:, Hb:2 * Hb], q2[:, 2 * Hb:], mask2, nseq, l1, l2, self.nh, self.pa2, rng)
+        x1 = self.d1.fwd(ctx2)
+        x2 = self.d2.fwd(ctx1)
+        yield
+        h1, t1s = self.t1.fwd(x1, s1, rng)
+        h2, t2s = self.t2.fwd(x2, s2, rng)
+        u1 = torch.empty((h1.shape[0], self.f1.i.W.shape[0]), dtype=h1.dtype, device=h1.device)
+        u2 = torch.empty((h2.shape[0], self.f2.i.W.shape[0]), dtype=h2.dtype, device=h2.device)
+        g1 = self.f1.i.fwd(h1, epi=L.EPI_BIAS_GELU, aux=u1)
+        g2 = self.f2.i.fwd(h2, epi=L.EPI_BIAS_GELU, aux=u2)
+        yield
+        o1 = self.f1.o.fwd(g1)
+        o2 = self.f2.o.fwd(g2)
+        yield
+        _, ts1 = self.f1.tail.fwd(o1, h1, rng, out=out1)
+        _, ts2 = self.f2.tail.fwd(o2, h2, rng, out=out2)
+        res.append((s1, s2, q1, q2, ctx1, ctx2, a1s, a2s, t1s, t2s, (h1, u1, g1, ts1), (h2, u2, g2, ts2), Hb))
+
+    def bwd_steps(self, dy1, dy2, saved, ds1, ds2):
+        s1, s2, q1, q2, ctx1, ctx2, a1s, a2s, t1s, t2s, f1s, f2s, Hb = saved
+        (h1, u1, g1, ts1), (h2, u2, g2, ts2) = f1s, f2s
+        dh1, dh2 = torch.empty_like(h1), torch.empty_like(h2)
+        do1 = self.f1.tail.bwd(dy1, ts1, dh1, dxsum=self.f1.o.gb)
+        do2 = self.f2.tail.bwd(dy2, ts2, dh2, dxsum=self.f2.o.gb)
+        self.f1.o.wgrad(do1, g1, bias_done=True)
+        self.f2.o.wgrad(do2, g2, bias_done=True)
+        du1 = self.f1.o.dgrad(do1, dgelu_aux=u1)
+        du2 = self.f2.o.dgrad(do2, dgelu_aux=u2)
+        yield
+        self.f1.i.wgrad(du1, h1)
+        self.f2.i.wgrad(du2, h2)
+        self.f1.i.dgrad(du1, dx=dh1, beta=1.0)
+        self.f2.i.dgrad(du2, dx=dh2, beta=1.0)
+        yield
+        da1 = self.t1.bwd(dh1, t1s, ds1, dxsum=self.d1.gb)
+        da2 = self.t2.bwd(dh2, t2s, ds2, dxsum=self.d2.gb)
+        self.d1.wgrad(da1, ctx2, bias_done=True)
+        self.d2.wgrad(da2, ctx1, bias_done=True)
+        dctx2 = self.d1.dgrad(da1)
+        dctx1 = self.d2.dgrad(da2)
+        yield
+        dq1 = torch.empty_like(q1)
+        dq2 = torch.empty_like(q2)
+        _attn_bwd(dctx1, ctx1, q2[:, 0:Hb], q1[:, Hb:2 * Hb], q1[:, 2 * Hb:], a1s, dq2[:, 0:Hb], dq1[:, Hb:2 * Hb],
+                  dq1[:, 2 * Hb:])
+        _attn_bwd(dctx2, ctx2, q1[:, 0:Hb], q2[:, Hb:2 * Hb], q2[:, 2 * Hb:], a2s, dq1[:, 0:Hb], dq2[:, Hb:2 * Hb],
+                  dq2[:, 2 * Hb:])
+        self.qkv1.wgrad(dq1, s1)
+        self.qkv2.wgrad(dq2, s2)
+        self.qkv1.dgrad(dq1, dx=ds1, beta=1.0)
+        self.qkv2.dgrad(dq2, dx=ds2, beta=1.0)
+
+
+GROUPED = os.environ.get("K3M_GROUPED", "1") != "0"
+
+
+def _lockstep(gens):
+    """Run generators segment by segment; each round's GEMMs are issued under one ops.grouped()."""
+    live = list(gens)
+    while live:
+        nxt = []
+        with ops.grouped():
+            for g in live:
+                try:
+                    next(g)
+                    nxt.append(g)
+                except StopIteration:
+                    pass
+        live = nxt
+
+
 def _ext_mask(m):
     # (1 - mask) * -10000 additive key mask (vilbert_k3m.py:2547-2580); input marshalling
     return ((1.0 - m.to(torch.float32)) * -10000.0).contiguous()
@@ -497,11 +579,17 @@ class K3MEngine(object):
                 ops_ = [self.co_tv[i], self.co_pv[i], self.co_tt[i]]
                 if not train:
                     ops_ = [_eval_view(o) for o in ops_]
-                s_tv = ops_[0].fwd(XV[0:BR], XT[0:BT], B, R, T, mask_v, mask_t, rng, XV2[0:BR], XT2[0:BT])
-                s_pv = ops_[1].fwd(XV[BR:], XT[2 * BT:2 * BT + BP], B, R, P, mask_v, mask_p, rng, XV2[BR:],
-                                   XT2[2 * BT:2 * BT + BP])
-                s_tt = ops_[2].fwd(XT[2 * BT + BP:], XT[BT:2 * BT], B, P, T, mask_p, mask_t, rng,
-                                   XT2[2 * BT + BP:], XT2[BT:2 * BT])
+                args = [(XV[0:BR], XT[0:BT], B, R, T, mask_v, mask_t, rng, XV2[0:BR], XT2[0:BT]),
+                        (XV[BR:], XT[2 * BT:2 * BT + BP], B, R, P, mask_v, mask_p, rng, XV2[BR:],
+                         XT2[2 * BT:2 * BT + BP]),
+                        (XT[2 * BT + BP:], XT[BT:2 * BT], B, P, T, mask_p, mask_t, rng, XT2[2 * BT + BP:],
+                         XT2[BT:2 * BT])]
+                if GROUPED:
+                    res = [[], [], []]
+                    _lockstep([o.fwd_steps(*a, res=r) for o, a, r in zip(ops_, args, res)])
+                    s_tv, s_pv, s_tt = res[0][0], res[1][0], res[2][0]
+                else:
+                    s_tv, s_pv, s_tt = [o.fwd(*a) for o, a in zip(ops_, args)]
                 enc.append((kind, i, (s_tv, s_pv, s_tt, ops_)))
                 XT, XV = XT2, XV2
         ctx["enc"] = enc
@@ -828,9 +916,14 @@ class K3MEngine(object):
                 s_tv, s_pv, s_tt, ops_ = sv
                 dXT2 = torch.empty_like(dXT)
                 dXV2 = torch.empty_like(dXV)
-                ops_[0].bwd(dXV[0:BR], dXT[0:BT], s_tv, dXV2[0:BR], dXT2[0:BT])
-                ops_[1].bwd(dXV[BR:], dXT[2 * BT:2 * BT + BP], s_pv, dXV2[BR:], dXT2[2 * BT:2 * BT + BP])
-                ops_[2].bwd(dXT[2 * BT + BP:], dXT[BT:2 * BT], s_tt, dXT2[2 * BT + BP:], dXT2[BT:2 * BT])
+                bargs = [(dXV[0:BR], dXT[0:BT], s_tv, dXV2[0:BR], dXT2[0:BT]),
+                         (dXV[BR:], dXT[2 * BT:2 * BT + BP], s_pv, dXV2[BR:], dXT2[2 * BT:2 * BT + BP]),
+                         (dXT[2 * BT + BP:], dXT[BT:2 * BT], s_tt, dXT2[2 * BT + BP:], dXT2[BT:2 * BT])]
+                if GROUPED:
+                    _lockstep([o.bwd_steps(*a) for o, a in zip(ops_, bargs)])
+                else:
+                    for o, a in zip(ops_, bargs):
+                        o.bwd(*a)
                 dXT, dXV = dXT2, dXV2
             if grad_ready is not None:
                 grad_ready(kind, i)

@@ -29,6 +29,48 @@ def empty(shape, like=None, dtype=torch.float32, device=None):
 F32_ALGO = {"x6": L.F32_SPLIT_BF16X6, "mfma": L.F32_MFMA_F32}[os.environ.get("K3M_F32_ALGO", "x6")]
 
 
+class _Grouper(object):
+    """Collects the GEMMs issued inside ``with grouped():`` and launches them on exit, one
+    k3m_gemm_grouped per kernel template (layout, epilogue, dtypes).  The GEMMs of one group must
+    be independent: nothing issued inside the block may read a GEMM output of the same block."""
+
+    def __init__(self):
+        self.pending = []
+
+    def flush(self):
+        groups = {}
+        for g, keep in self.pending:
+            key = (g.a_trans, g.b_trans, g.epilogue, g.dtype, g.c_dtype, g.f32_algo)
+            groups.setdefault(key, []).append((g, keep))
+        self.pending = []
+        for items in groups.values():
+            for i in range(0, len(items), GROUP_MAX):
+                chunk = items[i:i + GROUP_MAX]
+                arr = (L.K3mGemm * len(chunk))(*[g for g, _ in chunk])
+                call("k3m_gemm_grouped", L.C.cast(arr, L.C.c_void_p), len(chunk), stream())
+
+
+GROUP_MAX = 8
+_grouper = None
+
+
+class grouped(object):
+    """Context manager: defer and group the GEMMs issued inside (see _Grouper)."""
+
+    def __enter__(self):
+        global _grouper
+        assert _grouper is None, "grouped() does not nest"
+        _grouper = _Grouper()
+        return _grouper
+
+    def __exit__(self, *exc):
+        global _grouper
+        g, _grouper = _grouper, None
+        if exc[0] is None:
+            g.flush()
+        return False
+
+
 def gemm(a, a_trans, b, b_trans, c, m, n, k, epi=L.EPI_NONE, bias=None, aux=None, alpha=1.0, beta=0.0, splitk=1,
          ws=None, f32_algo=None):
     g = L.K3mGemm()
@@ -43,6 +85,9 @@ def gemm(a, a_trans, b, b_trans, c, m, n, k, epi=L.EPI_NONE, bias=None, aux=None
     g.a, g.b, g.c = ptr(a), ptr(b), ptr(c)
     g.bias, g.aux, g.ws = ptr(bias), ptr(aux), ptr(ws)
     g.alpha, g.beta = alpha, beta
+    if _grouper is not None:
+        _grouper.pending.append((g, (a, b, c, bias, aux, ws)))   # keep the tensors alive until the flush
+        return c
     call("k3m_gemm", L.C.byref(g), stream())
     return c
 

@@ -98,3 +98,54 @@ def test_x6_beta_all_tiles(dev, m, n, k, at, bt):
         ops.gemm(a, at, b, bt, c, m, n, k, alpha=0.5, beta=0.25, f32_algo=L.F32_SPLIT_BF16X6)
         err = float((c.double().cpu() - ref).abs().max())
         assert err < 2e-5 * float(ref.abs().max()), err
+
+
+def test_grouped_matches_individual():
+    """k3m_gemm_grouped (one grid over several problems) is bit-identical to launching each problem
+    through k3m_gemm: same tile computation, split-K slabs and epilogues."""
+    import torch
+    from k3m_amd import ops, _lib as L
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    cases = [  # (m, n, k, epi) nt forward problems of the co-attention blocks, ragged edges included
+        (2368, 3072, 1024, L.EPI_BIAS), (2304, 3072, 768, L.EPI_BIAS), (8192, 2304, 768, L.EPI_BIAS),
+        (300, 200, 96, L.EPI_BIAS), (2304, 1024, 1024, L.EPI_BIAS)]
+    for grouped in (False, True):
+        outs = []
+        torch.manual_seed(1)
+        ins = [(torch.randn(m, k, device=dev), torch.randn(n, k, device=dev) * 0.05, torch.randn(n, device=dev))
+               for m, n, k, _ in cases]
+        if grouped:
+            with ops.grouped():
+                for (x, w, b), (m, n, k, epi) in zip(ins, cases):
+                    outs.append(ops.linear(x, w, b))
+        else:
+            for (x, w, b), (m, n, k, epi) in zip(ins, cases):
+                outs.append(ops.linear(x, w, b))
+        torch.cuda.synchronize()
+        if not grouped:
+            ref = outs
+    for a, b in zip(outs, ref):
+        assert torch.equal(a, b)
+    # weight gradients (tn, split-K, beta = 1) and input gradients with the dGELU epilogue (nn)
+    dys = [torch.randn(20992 if i == 0 else 2304, n, device=dev) for i, n in enumerate((768, 1024, 3072))]
+    xs = [torch.randn(dy.shape[0], k, device=dev) for dy, k in zip(dys, (3072, 1024, 768))]
+    res = {}
+    for grouped in (False, True):
+        torch.manual_seed(2)
+        gws = [torch.ones(dy.shape[1], x.shape[1], device=dev) for dy, x in zip(dys, xs)]
+        ws_ = [torch.randn(dy.shape[1], x.shape[1], device=dev) * 0.05 for dy, x in zip(dys, xs)]
+        auxs = [torch.randn(dy.shape[0], x.shape[1], device=dev) for dy, x in zip(dys, xs)]
+        if grouped:
+            with ops.grouped():
+                for dy, x, gw in zip(dys, xs, gws):
+                    ops.linear_wgrad(dy, x, gw)
+                dxs = [ops.linear_dgrad(dy, w, dgelu_aux=a) for dy, w, a in zip(dys, ws_, auxs)]
+        else:
+            for dy, x, gw in zip(dys, xs, gws):
+                ops.linear_wgrad(dy, x, gw)
+            dxs = [ops.linear_dgrad(dy, w, dgelu_aux=a) for dy, w, a in zip(dys, ws_, auxs)]
+        torch.cuda.synchronize()
+        res[grouped] = (gws, dxs)
+    for a, b in zip(res[True][0] + res[True][1], res[False][0] + res[False][1]):
+        assert torch.equal(a, b)
