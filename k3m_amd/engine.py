@@ -23,6 +23,7 @@ Parameters and gradients live in one flat fp32 buffer each (k3m_amd/params.py); 
 gradients are accumulated in place by the GEMM epilogue (beta = 1) and bias/LN gradients by the
 reduction kernels, so there is no autograd bookkeeping on the hot path.
 """
+import contextlib
 import math
 import os
 
@@ -242,11 +243,12 @@ class BertLayerOp(object):
         qkv = self.qkv.fwd(x)
         ctx = torch.empty((M, H), dtype=x.dtype, device=x.device)
         asv = []
-        for (r0, nseq, ln, mask) in segs:
-            r1 = r0 + nseq * ln
-            _, s = _attn_fwd(qkv[r0:r1, 0:H], qkv[r0:r1, H:2 * H], qkv[r0:r1, 2 * H:], mask, nseq, ln, ln, self.nh,
-                             self.p_attn, rng, out=ctx[r0:r1])
-            asv.append(s)
+        with ops.branches():   # the sequence segments (text 36, PV 128) are independent launches
+            for (r0, nseq, ln, mask) in segs:
+                r1 = r0 + nseq * ln
+                _, s = ops.branch(_attn_fwd, qkv[r0:r1, 0:H], qkv[r0:r1, H:2 * H], qkv[r0:r1, 2 * H:], mask, nseq, ln,
+                                  ln, self.nh, self.p_attn, rng, out=ctx[r0:r1])
+                asv.append(s)
         a = self.o.fwd(ctx)
         h1, tsv = self.tail.fwd(a, x, rng)
         y, fsv = self.ffn.fwd(h1, rng)
@@ -261,10 +263,11 @@ class BertLayerOp(object):
         self.o.wgrad(da, ctx, bias_done=True)
         dctx = self.o.dgrad(da)
         dqkv = torch.empty_like(qkv)
-        for (r0, nseq, ln, mask), s in zip(segs, asv):
-            r1 = r0 + nseq * ln
-            _attn_bwd(dctx[r0:r1], ctx[r0:r1], qkv[r0:r1, 0:H], qkv[r0:r1, H:2 * H], qkv[r0:r1, 2 * H:], s,
-                      dqkv[r0:r1, 0:H], dqkv[r0:r1, H:2 * H], dqkv[r0:r1, 2 * H:])
+        with ops.branches():
+            for (r0, nseq, ln, mask), s in zip(segs, asv):
+                r1 = r0 + nseq * ln
+                ops.branch(_attn_bwd, dctx[r0:r1], ctx[r0:r1], qkv[r0:r1, 0:H], qkv[r0:r1, H:2 * H], qkv[r0:r1, 2 * H:],
+                           s, dqkv[r0:r1, 0:H], dqkv[r0:r1, H:2 * H], dqkv[r0:r1, 2 * H:])
         self.qkv.wgrad(dqkv, x)
         self.qkv.dgrad(dqkv, dx=dx, beta=1.0)
         return dx
@@ -380,8 +383,10 @@ class ConnectionOp(object):
         q1 = self.qkv1.fwd(s1)
         q2 = self.qkv2.fwd(s2)
         yield
-        ctx1, a1s = _attn_fwd(q2[:, 0:Hb], q1[:, Hb:2 * Hb], q1[:, 2 * Hb:], mask1, nseq, l2, l1, self.nh, self.pa1, rng)
-        ctx2, a2s = _attn_fwd(q1[:, 0:Hb], q2[:, Hb:2 * Hb], q2[:, 2 * Hb:], mask2, nseq, l1, l2, self.nh, self.pa2, rng)
+        ctx1, a1s = ops.branch(_attn_fwd, q2[:, 0:Hb], q1[:, Hb:2 * Hb], q1[:, 2 * Hb:], mask1, nseq, l2, l1, self.nh,
+                               self.pa1, rng)
+        ctx2, a2s = ops.branch(_attn_fwd, q1[:, 0:Hb], q2[:, Hb:2 * Hb], q2[:, 2 * Hb:], mask2, nseq, l1, l2, self.nh,
+                               self.pa2, rng)
         x1 = self.d1.fwd(ctx2)
         x2 = self.d2.fwd(ctx1)
         yield
@@ -424,10 +429,10 @@ class ConnectionOp(object):
         yield
         dq1 = torch.empty_like(q1)
         dq2 = torch.empty_like(q2)
-        _attn_bwd(dctx1, ctx1, q2[:, 0:Hb], q1[:, Hb:2 * Hb], q1[:, 2 * Hb:], a1s, dq2[:, 0:Hb], dq1[:, Hb:2 * Hb],
-                  dq1[:, 2 * Hb:])
-        _attn_bwd(dctx2, ctx2, q1[:, 0:Hb], q2[:, Hb:2 * Hb], q2[:, 2 * Hb:], a2s, dq1[:, 0:Hb], dq2[:, Hb:2 * Hb],
-                  dq2[:, 2 * Hb:])
+        ops.branch(_attn_bwd, dctx1, ctx1, q2[:, 0:Hb], q1[:, Hb:2 * Hb], q1[:, 2 * Hb:], a1s, dq2[:, 0:Hb],
+                   dq1[:, Hb:2 * Hb], dq1[:, 2 * Hb:])
+        ops.branch(_attn_bwd, dctx2, ctx2, q1[:, 0:Hb], q2[:, Hb:2 * Hb], q2[:, 2 * Hb:], a2s, dq1[:, 0:Hb],
+                   dq2[:, Hb:2 * Hb], dq2[:, 2 * Hb:])
         self.qkv1.wgrad(dq1, s1)
         self.qkv2.wgrad(dq2, s2)
         self.qkv1.dgrad(dq1, dx=ds1, beta=1.0)
@@ -437,6 +442,7 @@ class ConnectionOp(object):
 GROUPED = os.environ.get("K3M_GROUPED", "1") != "0"
 # text + image layer lock step: off by default — the text layers' GEMMs already fill the chip and the
 # mixed group measured 2.3 % slower (434.5 vs 444.6 samples/s, same box, A/B/A/B)
+GROUP_GATE = GROUPED and os.environ.get("K3M_GROUP_GATE", "1") != "0"   # the three fusion-gate GEMMs
 GROUP_TV = GROUPED and os.environ.get("K3M_GROUP_TV", "0") == "1"
 
 
@@ -446,12 +452,13 @@ def _lockstep(gens):
     while live:
         nxt = []
         with ops.grouped():
-            for g in live:
-                try:
-                    next(g)
-                    nxt.append(g)
-                except StopIteration:
-                    pass
+            with ops.branches():   # closes (main waits for the side streams) before the GEMM flush
+                for g in live:
+                    try:
+                        next(g)
+                        nxt.append(g)
+                    except StopIteration:
+                        pass
         live = nxt
 
 
@@ -688,14 +695,25 @@ class K3MEngine(object):
             "pv": (ind_pv, XT[2 * BT:2 * BT + BP], XT[2 * BT + BP:], seq_tp[BT:], H),
         }
         fus = {}
+        gate_a = {}
+        if mode == 1:   # the three modalities' gate GEMMs are independent: one grouped launch (GROUP_GATE)
+            ccs = {}
+            for m in ("v", "t", "pv"):
+                x0, x1, x2, out, D = streams[m]
+                rows = x0.shape[0]
+                cc = torch.empty((rows, 3 * D), dtype=torch.float32, device=dev)
+                L.call("k3m_relu_cat3", x0.data_ptr(), x1.data_ptr(), x2.data_ptr(), cc.data_ptr(), rows, D, L.F32,
+                       L.stream())
+                ccs[m] = (cc, self._lo(cc))
+            with (ops.grouped() if GROUP_GATE else contextlib.nullcontext()):
+                for m in ("v", "t", "pv"):
+                    gate_a[m] = self.gate[m].fwd(ccs[m][1], epi=L.EPI_BIAS_SIGMOID, out_dtype=torch.float32)
         for m in ("v", "t", "pv"):
             x0, x1, x2, out, D = streams[m]
             rows = x0.shape[0]
             if mode == 1:
-                cc = torch.empty((rows, 3 * D), dtype=torch.float32, device=dev)
-                L.call("k3m_relu_cat3", x0.data_ptr(), x1.data_ptr(), x2.data_ptr(), cc.data_ptr(), rows, D, L.F32,
-                       L.stream())
-                a = self.gate[m].fwd(self._lo(cc), epi=L.EPI_BIAS_SIGMOID, out_dtype=torch.float32)
+                cc = ccs[m][0]
+                a = gate_a[m]
                 ys = torch.empty_like(a)
                 idx = torch.empty((rows * D,), dtype=torch.uint8, device=dev)
                 nz = None
@@ -958,6 +976,22 @@ class K3MEngine(object):
             "t": (dXT[0:BT], dXT[BT:2 * BT], dseq_tp[0:BT]),
             "pv": (dXT[2 * BT:2 * BT + BP], dXT[2 * BT + BP:], dseq_tp[BT:]),
         }
+        gb = {}
+        if mode == 1:   # gate backward: elementwise part, then the three modalities' GEMMs grouped
+            for m in ("v", "t", "pv"):
+                rows, D = streams[m][0].shape[0], streams[m][4]
+                cc, a, ys, idx = fus[m]
+                dc = torch.empty_like(cc)
+                dpre = torch.empty_like(cc)
+                L.call("k3m_gate_bwd", dslices[m][2].data_ptr(), a.data_ptr(), cc.data_ptr(), ys.data_ptr(),
+                       idx.data_ptr(), dc.data_ptr(), dpre.data_ptr(), rows, D, L.F32, L.stream())
+                ops.colsum(dpre, self.gate[m].gb, accumulate=True)
+                gb[m] = (dc, dpre, self._lo(dpre), self._lo(cc))
+            with (ops.grouped() if GROUP_GATE else contextlib.nullcontext()):
+                for m in ("v", "t", "pv"):
+                    dc, dpre, dlo, clo = gb[m]
+                    self.gate[m].dgrad(dlo, dx=dc, beta=1.0)
+                    self.gate[m].wgrad(dlo, clo, bias_done=True)
         for m in ("v", "t", "pv"):
             x0 = streams[m][0]
             D = streams[m][4]
@@ -965,15 +999,8 @@ class K3MEngine(object):
             d1, d2, dout = dslices[m]
             d0 = torch.empty_like(x0)
             if mode == 1:
-                cc, a, ys, idx = fus[m]
-                dc = torch.empty_like(cc)
-                dpre = torch.empty_like(cc)
-                L.call("k3m_gate_bwd", dout.data_ptr(), a.data_ptr(), cc.data_ptr(), ys.data_ptr(), idx.data_ptr(),
-                       dc.data_ptr(), dpre.data_ptr(), rows, D, L.F32, L.stream())
-                dlo = self._lo(dpre)
-                self.gate[m].dgrad(dlo, dx=dc, beta=1.0)
-                self.gate[m].wgrad(dlo, self._lo(cc), bias_done=True)
-                ops.colsum(dpre, self.gate[m].gb, accumulate=True)
+                cc = fus[m][0]
+                dc = gb[m][0]
                 L.call("k3m_relu_split3_bwd", dc.data_ptr(), cc.data_ptr(), d0.data_ptr(), d1.data_ptr(), d2.data_ptr(),
                        rows, D, 0, L.F32, L.stream())
             else:

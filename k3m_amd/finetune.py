@@ -168,3 +168,37 @@ class ItemAlignmentTrainer(Trainer):
         self.optimizer_step(grad_scale=scale)
         eng.step_count += 1
         return {"item_embedding_1": e1, "item_embedding_2": e2, "probs": probs, "loss": loss}
+
+
+def evaluate(model, batches, thresholds=None):
+    """finetune.py:519-617 evaluation: the pair model in eval mode over ``batches`` (dicts with the
+    forward's argument names), probs collected on the host, precision / recall / F1 of
+    ``probs >= threshold`` for thresholds 0.1 .. 0.9.  (The reference concatenates with
+    ``np.concatenate(model_probs, probs)`` — the second argument is the axis, so it fails from the
+    second batch on; here the batches are concatenated.)"""
+    import numpy as np
+    from sklearn.metrics import f1_score, precision_score, recall_score
+    if thresholds is None:
+        thresholds = np.arange(0.1, 1.0, 0.1)
+    probs, labels = [], []
+    for pair in batches:
+        _, _, p, _ = model.forward(*[pair[k] for k in ARG_NAMES], train=False)
+        model._ctx = None   # no backward in evaluation
+        probs.append(p.detach().float().cpu().numpy())
+        labels.append(pair["labels"].detach().float().cpu().numpy())
+    probs = np.concatenate(probs) if probs else np.zeros(0)
+    labels = np.concatenate(labels) if labels else np.zeros(0)
+    out = []
+    for t in thresholds:
+        pred = probs >= t
+        out.append({"threshold": float(t),
+                    "precision": float(precision_score(labels, pred, zero_division=0)),
+                    "recall": float(recall_score(labels, pred, zero_division=0)),
+                    "f1": float(f1_score(labels, pred, zero_division=0))})
+    return out, probs, labels
+
+
+def save_model(model, path):
+    """The per-epoch ``K3M_item_alignment-<p>_epoch-<e>.bin`` (finetune.py:618-621): state_dict()."""
+    from .checkpoint import model_state_dict
+    torch.save(model_state_dict(model.engine.fp), path)

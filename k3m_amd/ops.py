@@ -36,14 +36,22 @@ class _Grouper(object):
 
     def __init__(self):
         self.pending = []
+        self.after = []   # non-GEMM work that must wait for the block's side-stream branches
 
     def flush(self):
+        after, self.after = self.after, []
+        for fn in after:
+            fn()
         groups = {}
         for g, keep in self.pending:
             key = (g.a_trans, g.b_trans, g.epilogue, g.dtype, g.c_dtype, g.f32_algo)
             groups.setdefault(key, []).append((g, keep))
         self.pending = []
-        for items in groups.values():
+        for key, items in groups.items():
+            if key[0] == 1 and not GROUP_WGRAD:   # weight gradients: each keeps its own split-K sizing
+                for g, _ in items:
+                    call("k3m_gemm", L.C.byref(g), stream())
+                continue
             for i in range(0, len(items), GROUP_MAX):
                 chunk = items[i:i + GROUP_MAX]
                 arr = (L.K3mGemm * len(chunk))(*[g for g, _ in chunk])
@@ -51,6 +59,7 @@ class _Grouper(object):
 
 
 GROUP_MAX = 8
+GROUP_WGRAD = os.environ.get("K3M_GROUP_WGRAD", "1") != "0"
 _grouper = None
 
 
@@ -69,6 +78,58 @@ class grouped(object):
         if exc[0] is None:
             g.flush()
         return False
+
+
+class branches(object):
+    """Context manager for independent launches on side streams: ``branch(fn, ...)`` inside runs fn
+    with a pool stream current (waiting first on everything the main stream issued before the
+    region); on exit the main stream waits for every branch.  Small launches that each leave most
+    CUs idle (one workgroup per (sequence, head) of a short attention) then overlap."""
+
+    _pool = {}
+
+    def __enter__(self):
+        global _branches
+        self.main = torch.cuda.current_stream()
+        dev = self.main.device
+        if dev not in branches._pool:
+            branches._pool[dev] = [torch.cuda.Stream(device=dev) for _ in range(max(1, BRANCH_STREAMS))]
+        self.streams = branches._pool[dev]
+        self.ev = torch.cuda.Event()
+        self.ev.record(self.main)
+        self.n = 0
+        self.waited = []
+        self.prev, _branches = _branches, self
+        return self
+
+    def __exit__(self, *exc):
+        global _branches
+        _branches = self.prev
+        for s in self.waited:
+            self.main.wait_stream(s)
+        return False
+
+    def run(self, fn, *args, **kw):
+        s = self.streams[self.n % len(self.streams)]
+        self.n += 1
+        if s not in self.waited:
+            s.wait_event(self.ev)
+            self.waited.append(s)
+        with torch.cuda.stream(s):
+            return fn(*args, **kw)
+
+
+# off by default: overlapping the short attention launches on side streams measured 3.7 % SLOWER
+# (423 vs 439 samples/s, same box) — kept selectable for other shapes (K3M_BRANCH_STREAMS=4)
+BRANCH_STREAMS = int(os.environ.get("K3M_BRANCH_STREAMS", "1"))
+_branches = None
+
+
+def branch(fn, *args, **kw):
+    """fn(*args) on a side stream inside ``with branches()``, inline otherwise."""
+    if _branches is None or BRANCH_STREAMS <= 1:
+        return fn(*args, **kw)
+    return _branches.run(fn, *args, **kw)
 
 
 def gemm(a, a_trans, b, b_trans, c, m, n, k, epi=L.EPI_NONE, bias=None, aux=None, alpha=1.0, beta=0.0, splitk=1,
@@ -144,7 +205,10 @@ def linear_wgrad(dy, x, gW, gb=None, alpha=1.0):
     ws = torch.empty((s * N * K,), dtype=torch.float32, device=dy.device) if s > 1 else None
     gemm(dy, 1, x, 0, gW, N, K, M, L.EPI_NONE, None, None, alpha, 1.0, s, ws)
     if gb is not None:
-        colsum(dy, gb, accumulate=True, alpha=alpha)
+        if _grouper is not None:   # dy may come from a side-stream branch of the same grouped block
+            _grouper.after.append(lambda: colsum(dy, gb, accumulate=True, alpha=alpha))
+        else:
+            colsum(dy, gb, accumulate=True, alpha=alpha)
 
 
 def colsum(x, out, accumulate=True, alpha=1.0):

@@ -120,3 +120,22 @@ def test_trainer_step_matches_oracle(dev):
             O.adamw_torch_step(p, G[n], m, v, 1, lr, 0.0 if is_no_decay(n) else 0.01)
         got = tr.engine.fp.p[n].cpu()
         np.testing.assert_allclose(got.numpy(), p.numpy(), rtol=1e-6, atol=1e-7 * lr / 1e-4, err_msg=n)
+
+
+def test_evaluate_and_save(dev, tmp_path):
+    """evaluate() runs the eval loop of finetune.py (precision/recall/F1 per threshold over several
+    batches) and save_model() writes the 989-key state_dict the reference saves per epoch."""
+    from k3m_amd.finetune import K3MForItemAlignment, evaluate, save_model
+    from k3m_amd.weights import param_values
+    g = load_ft_case("ce")
+    cfg = ft_config(g)
+    model = K3MForItemAlignment(cfg, dev)
+    model.engine.fp.load(param_values(cfg, int(g["weight_seed"])))
+    pair = {k: v.to(dev) for k, v in ft_pair(g).items()}
+    metrics, probs, labels = evaluate(model, [pair, pair])
+    assert len(metrics) == 9 and probs.shape == (4,) and labels.shape == (4,)
+    assert all(0.0 <= m["f1"] <= 1.0 for m in metrics)
+    path = str(tmp_path / "K3M_item_alignment-1_epoch-0.bin")
+    save_model(model, path)
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    assert len(sd) == 989 and "classifier.out_proj.weight" in sd
