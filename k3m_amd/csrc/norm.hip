@@ -120,51 +120,79 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
     pb[j] = floatx4{0.f, 0.f, 0.f, 0.f};
     px[j] = floatx4{0.f, 0.f, 0.f, 0.f};
   }
-  for (int row = blockIdx.x * 4 + w; row < rows; row += gridDim.x * 4) {
-    const long long base = (long long)row * cols;
-    floatx4 dyl[MAXV], xh[MAXV];
-    float s1 = 0.f, s2 = 0.f;
+  // two rows per wave and iteration: both rows' loads are in flight before either reduction
+  // (one row at a time left this HBM-bound kernel at ~0.44 of the bandwidth roofline)
+  const int S = gridDim.x * 4;
+  for (int row0 = blockIdx.x * 4 + w; row0 < rows; row0 += 2 * S) {
+    floatx4 dyl[2][MAXV], xh[2][MAXV];
+    float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < MAXV; ++j)
-      if (j < nv) {
-        const int c = (lane + 64 * j) * 4;
-        floatx4 d = ld4<T>(dy + base + c);
-        if (p_out > 0.f) {
+    for (int u = 0; u < 2; ++u) {
+      const int row = row0 + u * S;
+      const long long base = (long long)row * cols;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) d[q] *= k3m_dropout_scale(seed, off_out + base + c + q, p_out);
-        }
-        const floatx4 xv = ld4<T>(xhat + base + c);
-        dyl[j] = d;
-        xh[j] = xv;
-        pg[j] += d * xv;
-        pb[j] += d;
-        const floatx4 g = *reinterpret_cast<const floatx4*>(gamma + c);
-        const floatx4 dxh = d * g;
-        s1 += dxh[0] + dxh[1] + dxh[2] + dxh[3];
-        s2 += dxh[0] * xv[0] + dxh[1] * xv[1] + dxh[2] * xv[2] + dxh[3] * xv[3];
-      }
-    const float m1 = wave_sum(s1) / cols, m2 = wave_sum(s2) / cols;
-    const float rs = rstd[row];
-#pragma unroll
-    for (int j = 0; j < MAXV; ++j)
-      if (j < nv) {
-        const int c = (lane + 64 * j) * 4;
-        const floatx4 g = *reinterpret_cast<const floatx4*>(gamma + c);
-        floatx4 ds = (dyl[j] * g - m1 - xh[j] * m2) * rs;
-        floatx4 dr = ds;
-        if (acc_res) dr += ld4<T>(dres + base + c);
-        st4<T>(dres + base + c, dr);
-        if (dx != dres) {
-          if (p_in > 0.f) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) ds[q] *= k3m_dropout_scale(seed, off_in + base + c + q, p_in);
+      for (int j = 0; j < MAXV; ++j)
+        if (j < nv) {
+          const int c = (lane + 64 * j) * 4;
+          if (row < rows) {
+            dyl[u][j] = ld4<T>(dy + base + c);
+            xh[u][j] = ld4<T>(xhat + base + c);
+          } else {
+            dyl[u][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+            xh[u][j] = floatx4{0.f, 0.f, 0.f, 0.f};
           }
-          st4<T>(dx + base + c, ds);
         }
-        if (want_sum) {   // the sum of dx as stored (bf16-rounded when T is bf16)
-          px[j] += round4<T>(ds);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long long base = (long long)(row0 + u * S) * cols;
+#pragma unroll
+      for (int j = 0; j < MAXV; ++j)
+        if (j < nv) {
+          const int c = (lane + 64 * j) * 4;
+          floatx4 d = dyl[u][j];
+          if (p_out > 0.f) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) d[q] *= k3m_dropout_scale(seed, off_out + base + c + q, p_out);
+          }
+          dyl[u][j] = d;
+          const floatx4 xv = xh[u][j];
+          pg[j] += d * xv;     // rows past the end hold zeros: they add nothing
+          pb[j] += d;
+          const floatx4 g = *reinterpret_cast<const floatx4*>(gamma + c);
+          const floatx4 dxh = d * g;
+          s1[u] += dxh[0] + dxh[1] + dxh[2] + dxh[3];
+          s2[u] += dxh[0] * xv[0] + dxh[1] * xv[1] + dxh[2] * xv[2] + dxh[3] * xv[3];
         }
-      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int row = row0 + u * S;
+      const float m1 = wave_sum(s1[u]) / cols, m2 = wave_sum(s2[u]) / cols;
+      if (row >= rows) continue;
+      const long long base = (long long)row * cols;
+      const float rs = rstd[row];
+#pragma unroll
+      for (int j = 0; j < MAXV; ++j)
+        if (j < nv) {
+          const int c = (lane + 64 * j) * 4;
+          const floatx4 g = *reinterpret_cast<const floatx4*>(gamma + c);
+          floatx4 ds = (dyl[u][j] * g - m1 - xh[u][j] * m2) * rs;
+          floatx4 dr = ds;
+          if (acc_res) dr += ld4<T>(dres + base + c);
+          st4<T>(dres + base + c, dr);
+          if (dx != dres) {
+            if (p_in > 0.f) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) ds[q] *= k3m_dropout_scale(seed, off_in + base + c + q, p_in);
+            }
+            st4<T>(dx + base + c, ds);
+          }
+          if (want_sum) {   // the sum of dx as stored (bf16-rounded when T is bf16)
+            px[j] += round4<T>(ds);
+          }
+        }
+    }
   }
   // combine the 4 waves' column partials, write this block's slabs
   for (int k = 0; k < (want_sum ? 3 : 2); ++k) {
