@@ -108,8 +108,13 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_fwd_kernel(con
   const int hoff = h * hd;
   const long long pbase = ((long long)s * nh + h) * lq * lk;
 
-  stage<T, ML, NTH>(Qs, q, qrow0, ldq, hoff, LQ, lq, hd);
-  stage<T, ML, NTH>(KVs, k, krow0, ldk, hoff, LK, lk, hd);
+  {  // Q's and K's loads are issued together: one exposed global latency, not two
+    Chunks<T, ML, NTH> qch, kch;
+    stage_load(qch, q, qrow0, ldq, hoff, LQ, lq, hd);
+    stage_load(kch, k, krow0, ldk, hoff, LK, lk, hd);
+    stage_store(Qs, qch, LQ, hd);
+    stage_store(KVs, kch, LK, hd);
+  }
   __syncthreads();
   Chunks<T, ML, NTH> vch;  // V's loads fly while S is computed
   stage_load(vch, v, krow0, ldv, hoff, LK, lk, hd);
@@ -220,22 +225,28 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
   const int hoff = h * hd;
   const long long pbase = ((long long)s * nh + h) * lq * lk;
 
-  stage<T, ML, NTH>(R1, dctx, qrow0, ldc, hoff, LQ, lq, hd);
-  stage<T, ML, NTH>(R2, v, krow0, ldv, hoff, LK, lk, hd);
-  // D_i = dO_i . O_i: a wave per row, lanes over the head dimension (all loads issued first)
+  // D_i = dO_i . O_i: a wave per row, lanes over the head dimension.  dO's and V's staging loads
+  // and the D loads are all issued before any of them is used (one exposed global latency).
   {
     constexpr int RW = ML / NW;     // rows per wave
     float pa[RW][MAXD / 64], pb[RW][MAXD / 64];
+    {
+      Chunks<T, ML, NTH> c1, c2;
+      stage_load(c1, dctx, qrow0, ldc, hoff, LQ, lq, hd);
+      stage_load(c2, v, krow0, ldv, hoff, LK, lk, hd);
 #pragma unroll
-    for (int u = 0; u < RW; ++u) {
-      const int i = w + u * NW;
+      for (int u = 0; u < RW; ++u) {
+        const int i = w + u * NW;
 #pragma unroll
-      for (int c = 0; c < MAXD / 64; ++c) {
-        const int d = lane + 64 * c;
-        const bool ok = i < lq && d < hd;
-        pa[u][c] = ok ? to_f(dctx[(qrow0 + i) * ldc + hoff + d]) : 0.f;
-        pb[u][c] = ok ? to_f(o[(qrow0 + i) * ldo + hoff + d]) : 0.f;
+        for (int c = 0; c < MAXD / 64; ++c) {
+          const int d = lane + 64 * c;
+          const bool ok = i < lq && d < hd;
+          pa[u][c] = ok ? to_f(dctx[(qrow0 + i) * ldc + hoff + d]) : 0.f;
+          pb[u][c] = ok ? to_f(o[(qrow0 + i) * ldo + hoff + d]) : 0.f;
+        }
       }
+      stage_store(R1, c1, LQ, hd);
+      stage_store(R2, c2, LK, hd);
     }
 #pragma unroll
     for (int u = 0; u < RW; ++u) {
@@ -255,6 +266,13 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
     const int tq = LQ >> 5, tk = LK >> 5;
     for (int t = w; t < tq * tk; t += NW) {
       const int i0 = (t / tk) * 32, j0 = (t % tk) * 32;
+      const int j = j0 + cl;
+      float pr[16];   // this tile's probabilities: loaded before the MFMAs, which cover their latency
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = i0 + (r & 3) + 8 * (r >> 2) + 4 * kl;
+        pr[r] = (i < lq && j < lk) ? probs[pbase + (long long)i * lk + j] : 0.f;
+      }
       floatx16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -263,14 +281,13 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
         const float b = R2[sw(j0 + cl, kk + kl, hd)];
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
       }
-      const int j = j0 + cl;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = i0 + (r & 3) + 8 * (r >> 2) + 4 * kl;
         float ds = 0.f;
         if (i < lq && j < lk) {
           const long long pidx = pbase + (long long)i * lk + j;
-          ds = probs[pidx] * (acc[r] * k3m_dropout_scale(seed, off + pidx, p_drop) - Ds[i]);
+          ds = pr[r] * (acc[r] * k3m_dropout_scale(seed, off + pidx, p_drop) - Ds[i]);
         }
         R3[sw(i, j, LK)] = ds;
       }
@@ -280,6 +297,14 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
   stage_store(R2, nch, LK, hd);
   __syncthreads();
   stage_load(nch, q, qrow0, ldq, hoff, LQ, lq, hd);  // Q's loads fly during phases 2-3
+  constexpr int U = ML * ML / NTH;
+  float pv[U];   // phase 3's probabilities, loaded now: phase 2's MFMAs cover their latency
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = threadIdx.x + u * NTH;
+    const int i = e / LK, j = e - i * LK;
+    pv[u] = (e < LQ * LK && i < lq && j < lk) ? probs[pbase + (long long)i * lk + j] : 0.f;
+  }
   // phase 2: dQ = scale * dS K
   {
     const int tq = LQ >> 5, td = hd >> 5;
@@ -303,14 +328,6 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
   __syncthreads();
   // phase 3: R2 <- Pd [LQ][LK]; dV = Pd^T dO
   {
-    constexpr int U = ML * ML / NTH;
-    float pv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {   // all loads first
-      const int e = threadIdx.x + u * NTH;
-      const int i = e / LK, j = e - i * LK;
-      pv[u] = (e < LQ * LK && i < lq && j < lk) ? probs[pbase + (long long)i * lk + j] : 0.f;
-    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int e = threadIdx.x + u * NTH;

@@ -33,6 +33,9 @@ for s in "$@"; do
     pbf) step pbf 900 python -m pytest tests/test_gpu_parity.py -q -s -k bf16 ;;
     benchbf) step benchbf 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --dtype bf16 ;;
     attn) step attn 300 python scripts/attn_bench.py both ;;
+    apaths) step apaths 300 python scripts/attn_paths.py ;;
+    dcost) step dcost 300 python scripts/dropout_cost.py ;;
+    tattn) step tattn 600 python -u -m pytest tests -m gpu -k "attn or attention" -x -q --timeout 300 --timeout-method thread ;;
     tbf) step tbf 600 python -m pytest tests/test_gpu_gemm_bf16.py -q ;;
     ddp2) step ddp2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --backend gloo --batch 16 ;;
     pmc) export TMPDIR=/tmp
