@@ -21,6 +21,7 @@ namespace {
 
 constexpr int MAXL = 128;
 constexpr int MAXD = 128;
+constexpr float LOG2E = 1.4426950408889634f;
 // Two builds of each kernel: (ML = 128, 8 waves) for any sequence up to 128, and (ML = 64, 4 waves)
 // for sequences up to 64 (the text, image and text<->image co-attention cases: L = 36/37).  The
 // short build's register arrays are sized for 64 rows, so it holds ~half the VGPRs and, with its
@@ -28,6 +29,60 @@ constexpr int MAXD = 128;
 // one 8-wave workgroup per CU left most of each block's global-load and barrier waits exposed.
 
 __device__ __forceinline__ int sw(int i, int c, int cols) { return i * cols + (c ^ (i & 31)); }
+
+// acc += sum_k A(k) B(k) over k in [0, K) for one 32x32 tile, K a multiple of 16: lane operands
+// come from LDS through fa(k) / fb(k) (k already includes the lane's kl offset).  The next 16-wide
+// k slice's eight A and eight B reads are issued before the current slice's eight MFMAs, so the
+// LDS latency hides behind the matrix core instead of stalling every step.
+template <int S = 8, typename FA, typename FB>
+__device__ __forceinline__ void mfma_tile(floatx16& acc, int K, FA fa, FB fb) {
+  static_assert(S == 4 || S == 8, "slice of 4 or 8 MFMA steps (K is a multiple of 16)");
+  float a[S], b[S];
+#pragma unroll
+  for (int u = 0; u < S; ++u) {
+    a[u] = fa(2 * u);
+    b[u] = fb(2 * u);
+  }
+  for (int k0 = 0; k0 < K; k0 += 2 * S) {
+    float an[S], bn[S];
+    const int kn = k0 + 2 * S < K ? k0 + 2 * S : k0;  // last slice re-reads itself (unused, no branch)
+#pragma unroll
+    for (int u = 0; u < S; ++u) {
+      an[u] = fa(kn + 2 * u);
+      bn[u] = fb(kn + 2 * u);
+    }
+#pragma unroll
+    for (int u = 0; u < S; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < S; ++u) {
+      a[u] = an[u];
+      b[u] = bn[u];
+    }
+  }
+}
+
+// Phase timestamps for the lab build only (scripts/lab/attn_stamps.hip defines K3M_ATTN_STAMPS):
+// wave 0 of each workgroup records the 100 MHz wall clock at the phase boundaries.
+#ifdef K3M_ATTN_STAMPS
+__device__ unsigned long long k3m_attn_stamps[K3M_ATTN_STAMPS * 8];
+#define ATT_STAMP(n)                                                     \
+  do {                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < K3M_ATTN_STAMPS)                \
+      k3m_attn_stamps[blockIdx.x * 8 + (n)] = wall_clock64();            \
+  } while (0)
+#define ATT_STAMP_END(n) \
+  do {                   \
+    __syncthreads();     \
+    ATT_STAMP(n);        \
+  } while (0)
+#else
+#define ATT_STAMP(n) \
+  do {               \
+  } while (0)
+#define ATT_STAMP_END(n) \
+  do {                   \
+  } while (0)
+#endif
 
 // Staging HBM -> LDS in two halves so the loads of the next operand can be issued before the
 // current phase's MFMAs and written after its barrier: every thread loads its 16-byte chunks
@@ -88,6 +143,33 @@ __device__ __forceinline__ void stage(float* __restrict__ dst, const T* __restri
   stage_store(dst, ch, nrows, cols);
 }
 
+// dst[e] = <chunk e of a, chunk e of b> for every staged chunk e (row-major, cols/VE per row)
+template <typename T, int ML, int NTH>
+__device__ __forceinline__ void chunk_dots(float* __restrict__ dst, const Chunks<T, ML, NTH>& a,
+                                           const Chunks<T, ML, NTH>& b, int nrows, int cols) {
+  constexpr int VE = Chunks<T, ML, NTH>::VE;
+  const int nch = nrows * (cols / VE);
+#pragma unroll
+  for (int u = 0; u < Chunks<T, ML, NTH>::N; ++u) {
+    const int e = threadIdx.x + u * NTH;
+    if (e < nch) {
+      const uint32_t wa[4] = {a.r[u].x, a.r[u].y, a.r[u].z, a.r[u].w};
+      const uint32_t wb[4] = {b.r[u].x, b.r[u].y, b.r[u].z, b.r[u].w};
+      float acc = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if constexpr (VE == 8) {
+          acc += __uint_as_float(wa[q] << 16) * __uint_as_float(wb[q] << 16);
+          acc += __uint_as_float(wa[q] & 0xffff0000u) * __uint_as_float(wb[q] & 0xffff0000u);
+        } else {
+          acc += __uint_as_float(wa[q]) * __uint_as_float(wb[q]);
+        }
+      }
+      dst[e] = acc;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ forward
 template <typename T, int ML, int NW>
 __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_fwd_kernel(const T* __restrict__ q, long long ldq, const T* __restrict__ k,
@@ -103,11 +185,23 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_fwd_kernel(con
   float* Qs = smem;              // [LQ][hd]
   float* KVs = Qs + LQ * hd;     // [LK][hd]  K, then V
   float* Ss = KVs + LK * hd;     // [LQ][LK]  scores, then dropped probabilities
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: row math on the scalar unit
+  const int lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
   const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
   const int hoff = h * hd;
   const long long pbase = ((long long)s * nh + h) * lq * lk;
+  ATT_STAMP(0);
 
+  // additive key mask of the lane's key column in each 32-column tile (-inf on padding columns),
+  // loaded with Q and K: a load after the MFMAs would make the S phase wait for V's loads too
+  // (clamped addresses and no use before the S phase: the loads are issued unconditionally)
+  float mk[ML / 32];
+#pragma unroll
+  for (int t = 0; t < ML / 32; ++t) mk[t] = 0.f;
+  if (kmask) {
+#pragma unroll
+    for (int t = 0; t < ML / 32; ++t) mk[t] = kmask[krow0 + min(32 * t + cl, lk - 1)];
+  }
   {  // Q's and K's loads are issued together: one exposed global latency, not two
     Chunks<T, ML, NTH> qch, kch;
     stage_load(qch, q, qrow0, ldq, hoff, LQ, lq, hd);
@@ -116,6 +210,7 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_fwd_kernel(con
     stage_store(KVs, kch, LK, hd);
   }
   __syncthreads();
+  ATT_STAMP(1);
   Chunks<T, ML, NTH> vch;  // V's loads fly while S is computed
   stage_load(vch, v, krow0, ldv, hoff, LK, lk, hd);
   // S = scale * Q K^T + mask
@@ -126,52 +221,78 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_fwd_kernel(con
       floatx16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      for (int kk = 0; kk < hd; kk += 2) {
-        const float a = Qs[sw(i0 + cl, kk + kl, hd)];
-        const float b = KVs[sw(j0 + cl, kk + kl, hd)];
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
-      }
+      mfma_tile(acc, hd, [&](int kk) { return Qs[sw(i0 + cl, kk + kl, hd)]; },
+                [&](int kk) { return KVs[sw(j0 + cl, kk + kl, hd)]; });
       const int j = j0 + cl;
-      const float mj = j < lk ? (kmask ? kmask[krow0 + j] : 0.f) : -INFINITY;
+      const float mj = j < lk ? mk[j0 >> 5] * LOG2E : -INFINITY;
+      const float sl = scale * LOG2E;   // scores kept in log2 units: softmax uses exp2
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = i0 + (r & 3) + 8 * (r >> 2) + 4 * kl;
-        Ss[sw(i, j, LK)] = acc[r] * scale + mj;
+        Ss[sw(i, j, LK)] = acc[r] * sl + mj;
       }
     }
   }
   __syncthreads();
+  ATT_STAMP(2);
   stage_store(KVs, vch, LK, hd);  // K no longer needed
-  // softmax rows (wave per row, lanes over keys), dropout, save P
-  for (int i = w; i < LQ; i += NW) {
-    const float x0 = lane < LK ? Ss[sw(i, lane, LK)] : -INFINITY;
-    const float x1 = lane + 64 < LK ? Ss[sw(i, lane + 64, LK)] : -INFINITY;
-    const float mx = wave_max(fmaxf(x0, x1));
-    float e0 = lane < lk ? expf(x0 - mx) : 0.f;
-    float e1 = lane + 64 < lk ? expf(x1 - mx) : 0.f;
-    const float inv = 1.f / wave_sum(e0 + e1);
-    e0 *= inv;
-    e1 *= inv;
-    const bool act = i < lq;
-    const long long prow = pbase + (long long)i * lk;
-    if (lane < LK) {
-      float pd = 0.f;
-      if (act && lane < lk) {
-        probs[prow + lane] = e0;
-        pd = e0 * k3m_dropout_scale(seed, off + prow + lane, p_drop);
+  // softmax rows (wave per row, lanes over keys), dropout, save P.  A wave takes its rows in
+  // groups of G: the G reductions are independent shuffle chains that overlap.  Rows >= lq (the
+  // zero-padded queries) are skipped: their S rows stay as they are, and the PV rows they feed
+  // are never stored.
+  ATT_STAMP(3);
+  {
+    constexpr int RW = ML / NW, G = 4;
+    constexpr bool TWO = ML > 64;   // keys lane + 64 exist only in the 128-row build
+    const K3mDrop dr = k3m_drop_init(seed, p_drop);
+    for (int g = 0; g < RW; g += G) {
+      if (w + g * NW >= lq) break;   // wave-uniform
+      float x0[G], x1[G], mx[G], sm[G];
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        const int i = min(w + (g + u) * NW, LQ - 1);   // rows past lq: computed, never stored
+        x0[u] = lane < LK ? Ss[sw(i, lane, LK)] : -INFINITY;
+        x1[u] = TWO && lane + 64 < LK ? Ss[sw(i, lane + 64, LK)] : -INFINITY;
+        mx[u] = fmaxf(x0[u], x1[u]);
       }
-      Ss[sw(i, lane, LK)] = pd;
-    }
-    if (lane + 64 < LK) {
-      float pd = 0.f;
-      if (act && lane + 64 < lk) {
-        probs[prow + lane + 64] = e1;
-        pd = e1 * k3m_dropout_scale(seed, off + prow + lane + 64, p_drop);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int u = 0; u < G; ++u) mx[u] = fmaxf(mx[u], __shfl_xor(mx[u], o, 64));
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        x0[u] = lane < lk ? exp2f(x0[u] - mx[u]) : 0.f;
+        x1[u] = TWO && lane + 64 < lk ? exp2f(x1[u] - mx[u]) : 0.f;
+        sm[u] = x0[u] + x1[u];
       }
-      Ss[sw(i, lane + 64, LK)] = pd;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int u = 0; u < G; ++u) sm[u] += __shfl_xor(sm[u], o, 64);
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        const int i = w + (g + u) * NW;   // wave-uniform
+        if (i >= lq) break;
+        const float inv = __builtin_amdgcn_rcpf(sm[u]);
+        const long long prow = pbase + (long long)i * lk;
+        // values computed unconditionally; only the stores are predicated
+        const float e0 = x0[u] * inv;
+        const bool ok0 = lane < lk;
+        const float pd0 = ok0 ? e0 * k3m_drop(dr, off + prow + lane) : 0.f;
+        if (ok0) probs[prow + lane] = e0;
+        if (lane < LK) Ss[sw(i, lane, LK)] = pd0;
+        if (TWO) {
+          const float e1 = x1[u] * inv;
+          const bool ok1 = lane + 64 < lk;
+          const float pd1 = ok1 ? e1 * k3m_drop(dr, off + prow + lane + 64) : 0.f;
+          if (ok1) probs[prow + lane + 64] = e1;
+          if (lane + 64 < LK) Ss[sw(i, lane + 64, LK)] = pd1;
+        }
+      }
     }
   }
   __syncthreads();
+  ATT_STAMP(4);
   // O = Pd V
   {
     const int tq = LQ >> 5, td = hd >> 5;
@@ -180,11 +301,8 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_fwd_kernel(con
       floatx16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      for (int kk = 0; kk < LK; kk += 2) {
-        const float a = Ss[sw(i0 + cl, kk + kl, LK)];
-        const float b = KVs[sw(kk + kl, d0 + cl, hd)];
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
-      }
+      mfma_tile(acc, LK, [&](int kk) { return Ss[sw(i0 + cl, kk + kl, LK)]; },
+                [&](int kk) { return KVs[sw(kk + kl, d0 + cl, hd)]; });
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = i0 + (r & 3) + 8 * (r >> 2) + 4 * kl;
@@ -192,6 +310,7 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_fwd_kernel(con
       }
     }
   }
+  ATT_STAMP_END(5);
 }
 
 // ------------------------------------------------------------------ backward
@@ -210,6 +329,7 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
                                                        long long lddk, long long lddv, int lq, int lk, int nh, int hd,
                                                        float scale, float p_drop, uint64_t seed, uint64_t off) {
   constexpr int NTH = NW * 64;
+  constexpr int BS = 4;   // MFMA slice depth of the backward's products (register budget)
   extern __shared__ float smem[];
   const int s = blockIdx.x / nh, h = blockIdx.x % nh;
   const int LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
@@ -220,45 +340,37 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
   // D_i is needed only until phase 1 ends, while R2 still holds V: keep it in R2's spare tail
   // when there is one (the L=128, d=64 case uses exactly 160 KiB that way)
   float* Ds = (LK * hd + LQ <= r2n) ? R2 + LK * hd : R3 + LQ * LK;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: row math on the scalar unit
+  const int lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
   const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
   const int hoff = h * hd;
   const long long pbase = ((long long)s * nh + h) * lq * lk;
+  const K3mDrop dr = k3m_drop_init(seed, p_drop);
+  ATT_STAMP(0);
 
-  // D_i = dO_i . O_i: a wave per row, lanes over the head dimension.  dO's and V's staging loads
-  // and the D loads are all issued before any of them is used (one exposed global latency).
+  // D_i = dO_i . O_i.  dO's, V's and O's 16-byte chunks are loaded together (one exposed global
+  // latency); each thread writes the dot product of its dO and O chunks into R3 (free until
+  // phase 1), then one thread per row adds its row's chunk dots in a fixed order.
   {
-    constexpr int RW = ML / NW;     // rows per wave
-    float pa[RW][MAXD / 64], pb[RW][MAXD / 64];
-    {
-      Chunks<T, ML, NTH> c1, c2;
-      stage_load(c1, dctx, qrow0, ldc, hoff, LQ, lq, hd);
-      stage_load(c2, v, krow0, ldv, hoff, LK, lk, hd);
-#pragma unroll
-      for (int u = 0; u < RW; ++u) {
-        const int i = w + u * NW;
-#pragma unroll
-        for (int c = 0; c < MAXD / 64; ++c) {
-          const int d = lane + 64 * c;
-          const bool ok = i < lq && d < hd;
-          pa[u][c] = ok ? to_f(dctx[(qrow0 + i) * ldc + hoff + d]) : 0.f;
-          pb[u][c] = ok ? to_f(o[(qrow0 + i) * ldo + hoff + d]) : 0.f;
-        }
-      }
-      stage_store(R1, c1, LQ, hd);
-      stage_store(R2, c2, LK, hd);
-    }
-#pragma unroll
-    for (int u = 0; u < RW; ++u) {
+    Chunks<T, ML, NTH> c1, c2, c3;
+    stage_load(c1, dctx, qrow0, ldc, hoff, LQ, lq, hd);
+    stage_load(c2, v, krow0, ldv, hoff, LK, lk, hd);
+    stage_load(c3, o, qrow0, ldo, hoff, LQ, lq, hd);
+    stage_store(R1, c1, LQ, hd);
+    stage_store(R2, c2, LK, hd);
+    chunk_dots<T, ML, NTH>(R3, c1, c3, LQ, hd);
+  }
+  __syncthreads();
+  {
+    const int cpr = hd / Chunks<T, ML, NTH>::VE;
+    if (threadIdx.x < LQ) {
       float a = 0.f;
-#pragma unroll
-      for (int c = 0; c < MAXD / 64; ++c) a += pa[u][c] * pb[u][c];
-      a = wave_sum(a);
-      const int i = w + u * NW;
-      if (lane == 0 && i < LQ) Ds[i] = a;
+      for (int c = 0; c < cpr; ++c) a += R3[threadIdx.x * cpr + c];
+      Ds[threadIdx.x] = a;
     }
   }
   __syncthreads();
+  ATT_STAMP(1);
   Chunks<T, ML, NTH> nch;  // K's loads fly during phase 1
   stage_load(nch, k, krow0, ldk, hoff, LK, lk, hd);
   // phase 1: dS
@@ -276,24 +388,18 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
       floatx16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      for (int kk = 0; kk < hd; kk += 2) {
-        const float a = R1[sw(i0 + cl, kk + kl, hd)];
-        const float b = R2[sw(j0 + cl, kk + kl, hd)];
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
-      }
+      mfma_tile<BS>(acc, hd, [&](int kk) { return R1[sw(i0 + cl, kk + kl, hd)]; },
+                [&](int kk) { return R2[sw(j0 + cl, kk + kl, hd)]; });
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = i0 + (r & 3) + 8 * (r >> 2) + 4 * kl;
-        float ds = 0.f;
-        if (i < lq && j < lk) {
-          const long long pidx = pbase + (long long)i * lk + j;
-          ds = pr[r] * (acc[r] * k3m_dropout_scale(seed, off + pidx, p_drop) - Ds[i]);
-        }
-        R3[sw(i, j, LK)] = ds;
+        const float ds = pr[r] * (acc[r] * k3m_drop(dr, off + pbase + (long long)i * lk + j) - Ds[i]);
+        R3[sw(i, j, LK)] = (i < lq && j < lk) ? ds : 0.f;
       }
     }
   }
   __syncthreads();
+  ATT_STAMP(2);
   stage_store(R2, nch, LK, hd);
   __syncthreads();
   stage_load(nch, q, qrow0, ldq, hoff, LQ, lq, hd);  // Q's loads fly during phases 2-3
@@ -313,11 +419,8 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
       floatx16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      for (int kk = 0; kk < LK; kk += 2) {
-        const float a = R3[sw(i0 + cl, kk + kl, LK)];
-        const float b = R2[sw(kk + kl, d0 + cl, hd)];
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
-      }
+      mfma_tile<BS>(acc, LK, [&](int kk) { return R3[sw(i0 + cl, kk + kl, LK)]; },
+                [&](int kk) { return R2[sw(kk + kl, d0 + cl, hd)]; });
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = i0 + (r & 3) + 8 * (r >> 2) + 4 * kl;
@@ -326,6 +429,7 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
     }
   }
   __syncthreads();
+  ATT_STAMP(3);
   // phase 3: R2 <- Pd [LQ][LK]; dV = Pd^T dO
   {
 #pragma unroll
@@ -333,7 +437,7 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
       const int e = threadIdx.x + u * NTH;
       if (e < LQ * LK) {
         const int i = e / LK, j = e - i * LK;
-        R2[sw(i, j, LK)] = pv[u] * k3m_dropout_scale(seed, off + pbase + (long long)i * lk + j, p_drop);
+        R2[sw(i, j, LK)] = pv[u] * k3m_drop(dr, off + pbase + (long long)i * lk + j);
       }
     }
   }
@@ -345,11 +449,8 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
       floatx16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      for (int kk = 0; kk < LQ; kk += 2) {
-        const float a = R2[sw(kk + kl, j0 + cl, LK)];   // A[j][i] = Pd[i][j]
-        const float b = R1[sw(kk + kl, d0 + cl, hd)];   // dO[i][d]
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
-      }
+      mfma_tile<BS>(acc, LQ, [&](int kk) { return R2[sw(kk + kl, j0 + cl, LK)]; },    // A[j][i] = Pd[i][j]
+                [&](int kk) { return R1[sw(kk + kl, d0 + cl, hd)]; });          // dO[i][d]
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int j = j0 + (r & 3) + 8 * (r >> 2) + 4 * kl;
@@ -358,6 +459,7 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
     }
   }
   __syncthreads();
+  ATT_STAMP(4);
   // phase 4: R1 <- Q; dK = scale * dS^T Q
   stage_store(R1, nch, LQ, hd);
   __syncthreads();
@@ -368,11 +470,8 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
       floatx16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      for (int kk = 0; kk < LQ; kk += 2) {
-        const float a = R3[sw(kk + kl, j0 + cl, LK)];   // A[j][i] = dS[i][j]
-        const float b = R1[sw(kk + kl, d0 + cl, hd)];   // Q[i][d]
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
-      }
+      mfma_tile<BS>(acc, LQ, [&](int kk) { return R3[sw(kk + kl, j0 + cl, LK)]; },    // A[j][i] = dS[i][j]
+                [&](int kk) { return R1[sw(kk + kl, d0 + cl, hd)]; });          // Q[i][d]
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int j = j0 + (r & 3) + 8 * (r >> 2) + 4 * kl;
@@ -380,6 +479,7 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
       }
     }
   }
+  ATT_STAMP_END(5);
 }
 
 size_t fwd_lds(int lq, int lk, int hd) {

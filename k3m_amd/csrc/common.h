@@ -37,19 +37,54 @@ template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float v) {
 // ---------------------------------------------------------------- counter-based RNG
 // Stateless: every dropout / gumbel site draws u(seed, offset + element) so the backward pass
 // regenerates the forward mask instead of storing it.
-__device__ __forceinline__ uint32_t k3m_hash(uint64_t seed, uint64_t ctr) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (ctr + 1ull);
+//
+// Cost matters: the attention softmax and LayerNorm tails draw one value per element.  The 64-bit
+// seed is expanded once per launch (splitmix64 of a kernel argument: wave-uniform, scalar ALU);
+// per element the counter's high word is folded in with one multiply and the low word goes
+// through Wellons' "lowbias32" finaliser (two multiplies, full avalanche).  That is 3 32-bit
+// multiplies per element instead of the 12 of a per-element splitmix64.
+__device__ __forceinline__ uint32_t k3m_mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint64_t k3m_seed_key(uint64_t seed) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (uint32_t)(z >> 32);
+  return z ^ (z >> 31);
 }
-// keep with probability (1-p): returns scale 1/(1-p) or 0.
+__device__ __forceinline__ uint32_t k3m_hash_key(uint64_t key, uint64_t ctr) {
+  const uint32_t lo = (uint32_t)ctr, hi = (uint32_t)(ctr >> 32);
+  return k3m_mix32(lo ^ (uint32_t)key ^ ((hi ^ (uint32_t)(key >> 32)) * 0x9E3779B1u));
+}
+__device__ __forceinline__ uint32_t k3m_hash(uint64_t seed, uint64_t ctr) {
+  return k3m_hash_key(k3m_seed_key(seed), ctr);
+}
+// Dropout with keep probability (1-p): scale 1/(1-p) or 0.  An element is kept iff
+// u = (h >> 8) * 2^-24 >= p, i.e. iff (h >> 8) >= thr = ceil(p * 2^24) (p * 2^24 is exact in fp32),
+// so the test is one integer compare.  Set up once per launch (wave-uniform) with k3m_drop_init.
+struct K3mDrop {
+  uint64_t key;
+  uint32_t thr;   // 0: p == 0, nothing dropped
+  float scale;
+};
+__device__ __forceinline__ K3mDrop k3m_drop_init(uint64_t seed, float p) {
+  K3mDrop d;
+  d.key = k3m_seed_key(seed);
+  d.thr = p > 0.f ? (uint32_t)ceilf(p * 16777216.0f) : 0u;
+  d.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  return d;
+}
+__device__ __forceinline__ float k3m_drop(const K3mDrop& d, uint64_t ctr) {
+  if (d.thr == 0u) return 1.f;
+  return (k3m_hash_key(d.key, ctr) >> 8) >= d.thr ? d.scale : 0.f;
+}
 __device__ __forceinline__ float k3m_dropout_scale(uint64_t seed, uint64_t ctr, float p) {
-  if (p <= 0.f) return 1.f;
-  uint32_t h = k3m_hash(seed, ctr);
-  float u = (float)(h >> 8) * (1.0f / 16777216.0f);
-  return u >= p ? 1.f / (1.f - p) : 0.f;
+  return k3m_drop(k3m_drop_init(seed, p), ctr);
 }
 // uniform in the OPEN interval (0, 1): both log(u) and log(-log(u)) stay finite (gumbel noise)
 __device__ __forceinline__ float k3m_uniform(uint64_t seed, uint64_t ctr) {
