@@ -2,7 +2,7 @@
 // K3M_ATTN_STAMPS: wave 0 of every workgroup stamps the 100 MHz wall clock at each phase boundary).
 // Prints, per shape, the kernel's span, the mean workgroup lifetime, the mean duration of each
 // phase and how many workgroups were resident on average (sum of lifetimes / span).
-//   ./attn_stamps                       (the wide engine's shapes, fp32, dropout 0.1)
+//   ./attn_stamps [shape index]         (the wide engine's shapes, fp32, dropout 0.1)
 #define K3M_ATTN_STAMPS 8192
 #include "../../k3m_amd/csrc/attention.hip"
 
@@ -52,14 +52,17 @@ static void report(const char* what, int nblk, int nst, const char* const* names
   std::printf("\n");
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const int only = argc > 1 ? std::atoi(argv[1]) : -1;
   const int shapes[][5] = {{128, 128, 128, 12, 64}, {128, 36, 36, 12, 64}, {128, 37, 37, 8, 128},
                            {64, 128, 37, 8, 128},  {64, 37, 128, 8, 128}};
   const char* fn[] = {"stage_QK", "S", "V(w0)", "softmax", "PV"};
   const char* bn[] = {"stage+D", "dS", "K+dQ", "Pd+dV", "Q+dK"};
   hipStream_t st;
   CK(hipStreamCreate(&st));
-  for (auto& sh : shapes) {
+  for (int si = 0; si < (int)(sizeof(shapes) / sizeof(shapes[0])); ++si) {
+    if (only >= 0 && si != only) continue;
+    const int* sh = shapes[si];
     const int nseq = sh[0], lq = sh[1], lk = sh[2], nh = sh[3], hd = sh[4], D = nh * hd;
     float* q = dev_rand((size_t)nseq * lq * D, 1);
     float* k = dev_rand((size_t)nseq * lk * D, 2);

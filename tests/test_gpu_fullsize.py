@@ -2,8 +2,9 @@
 P=128, R=37, 10 triples), where the CPU oracle is too slow to compare against directly.
 
 * the default fp32 path (bf16x6 GEMMs) and the exact-f32 MFMA path compute the same step: every
-  loss within 1e-4 relative, c_final within 1e-3, total gradient norm within 1e-4 and every
-  parameter's gradient norm within 1e-3 relative (+ a floor for ~0 gradients);
+  loss within 1e-4 relative, c_final within 1e-3 (but for rare near-tie flips of the hard gumbel
+  gate), total gradient norm within 1e-4 and every parameter's gradient norm within 1e-3 relative
+  (+ a floor for ~0 gradients);
 * the step is reproducible: two eval-mode steps on the same inputs give bitwise-identical losses and
   forward outputs, and gradients equal to fp32 rounding (float atomics in two backward kernels);
 * a train-mode full-size step (dropout, device gumbel noise and negatives, AdamW) is finite.
@@ -69,7 +70,11 @@ def test_fullsize_x6_matches_exact_f32(setup):
     lf, cf, gf = _run(setup, L.F32_MFMA_F32)
     assert np.all(np.isfinite(l6)), l6
     np.testing.assert_allclose(l6, lf, rtol=1e-4, atol=1e-6)
-    torch.testing.assert_close(c6, cf, rtol=1e-3, atol=1e-4)
+    # c_final comes out of the hard (argmax) gumbel gate: where two gate logits are within the
+    # GEMMs' rounding difference of a tie, the two algorithms may pick different sources for that
+    # channel.  Such flips must stay rare; every other element agrees to 1e-3.
+    bad = ~torch.isclose(c6, cf, rtol=1e-3, atol=1e-4)
+    assert int(bad.sum()) <= max(8, c6.numel() // 2000), (int(bad.sum()), c6.numel())
     n6, nf = float(g6.double().norm()), float(gf.double().norm())
     assert abs(n6 - nf) <= 1e-4 * nf, (n6, nf)
     eng = setup[1]
