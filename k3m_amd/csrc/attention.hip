@@ -17,6 +17,8 @@
 // context = P.V, heads concatenated along the hidden dimension.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int MAXL = 128;
@@ -482,6 +484,201 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
   ATT_STAMP_END(5);
 }
 
+// ------------------------------------------------------------------ forward, probabilities in registers
+// fp32, lq, lk <= 128, K and V of the head in LDS (<= 80 KB: two or more workgroups per CU).  One
+// wave per 32-query block, the queries on the MFMA lanes:
+//   S^T = K Q^T    A = K from LDS (16-byte reads; lane half kl takes head dims [kl*HD/2, (kl+1)*HD/2)
+//                  — the k order of a dot product is free), B = this wave's Q block held in
+//                  registers (prescaled by scale*log2e), accumulators started at the key mask;
+//   softmax        in the accumulators: lane (query q, half kl) holds keys 32kt + crow(r, kl), so a
+//                  query's max and sum are 64 in-lane operations plus one exchange with lane ^ 32;
+//   O^T = V^T P^T  B = the dropped probabilities straight from the accumulators (step s of key tile
+//                  kt takes key 32kt + crow(s, kl) on both operands), A = V from LDS at
+//                  compile-time offsets;
+//   ctx            lane (q, kl) holds O[q][32dt + crow(r, kl)]: 16-byte stores.
+// No S or P image in LDS, one barrier per workgroup.  crow(r, kl) = (r & 3) + 8 (r >> 2) + 4 kl.
+template <int HD>
+__global__ __launch_bounds__(256, 2) void attn_fwd_reg_kernel(const float* __restrict__ q, long long ldq,
+                                                              const float* __restrict__ k, long long ldk,
+                                                              const float* __restrict__ v, long long ldv,
+                                                              const float* __restrict__ kmask, float* __restrict__ ctx,
+                                                              long long ldc, float* __restrict__ probs, int lq, int lk,
+                                                              int nh, float scale, float p_drop, uint64_t seed,
+                                                              uint64_t off) {
+  constexpr int NTH = 256, HH = HD / 2, NCH = HD / 4;
+  constexpr int SWZ = (HD % 64 == 0) ? 15 : 7;   // XOR of the 16-byte chunk index by the key row
+  constexpr int U = 8192 / 4 / NTH;               // staging chunks per thread and operand (LK*HD <= 8192)
+  extern __shared__ float smem[];
+  const int s = blockIdx.x / nh, h = blockIdx.x % nh;
+  const int LK = (lk + 31) & ~31, nkt = LK >> 5;
+  float* Ks = smem;              // [LK][HD], chunk c of row j stored at chunk c ^ (j & SWZ)
+  float* Vs = Ks + LK * HD;      // [LK][HD]
+  float* mk = Vs + LK * HD;      // [LK]: key mask in log2 units, -inf on padding keys
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
+  const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
+  const int hoff = h * HD;
+  const long long pbase = ((long long)s * nh + h) * lq * lk;
+  const int qi = 32 * w + cl;    // this lane's query
+  ATT_STAMP(0);
+
+  // staging: K, V chunks and the mask (all loads first), and the wave's Q block into registers
+  {
+    float4 kc[U], vc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = threadIdx.x + u * NTH, j = e / NCH, c = e % NCH;
+      const bool ok = e < LK * NCH && j < lk;
+      const long long row = krow0 + (ok ? j : 0);
+      kc[u] = ok ? *reinterpret_cast<const float4*>(k + row * ldk + hoff + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      vc[u] = ok ? *reinterpret_cast<const float4*>(v + row * ldv + hoff + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float mv = 0.f;
+    if (threadIdx.x < LK && kmask) mv = kmask[krow0 + min((int)threadIdx.x, lk - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = threadIdx.x + u * NTH, j = e / NCH, c = e % NCH;
+      if (e < LK * NCH) {
+        *reinterpret_cast<float4*>(Ks + j * HD + 4 * (c ^ (j & SWZ))) = kc[u];
+        *reinterpret_cast<float4*>(Vs + j * HD + 4 * c) = vc[u];
+      }
+    }
+    if (threadIdx.x < LK) mk[threadIdx.x] = (int)threadIdx.x < lk ? mv * LOG2E : -INFINITY;
+  }
+  float qr[HH];
+  {
+    const float sl = scale * LOG2E;
+    const bool ok = qi < lq;
+    const float* src = q + (qrow0 + (ok ? qi : 0)) * ldq + hoff + kl * HH;
+#pragma unroll
+    for (int c = 0; c < HH / 4; ++c) {
+      const float4 t = ok ? *reinterpret_cast<const float4*>(src + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      qr[4 * c] = t.x * sl;
+      qr[4 * c + 1] = t.y * sl;
+      qr[4 * c + 2] = t.z * sl;
+      qr[4 * c + 3] = t.w * sl;
+    }
+  }
+  __syncthreads();
+  ATT_STAMP(1);
+  if (32 * w >= lq) return;   // no queries for this wave (no barrier follows)
+
+  // S^T tiles, started at the key mask
+  floatx16 acc[4];
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) {
+    if (kt < nkt) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const float4 m4 = *reinterpret_cast<const float4*>(mk + 32 * kt + 8 * a + 4 * kl);
+        acc[kt][4 * a] = m4.x;
+        acc[kt][4 * a + 1] = m4.y;
+        acc[kt][4 * a + 2] = m4.z;
+        acc[kt][4 * a + 3] = m4.w;
+      }
+      const int key = 32 * kt + cl;
+      const float* krow = Ks + key * HD;
+      const int sw = key & SWZ;
+#pragma unroll
+      for (int m = 0; m < HH; m += 4) {
+        const float4 a4 = *reinterpret_cast<const float4*>(krow + 4 * (((kl * HH + m) >> 2) ^ sw));
+        acc[kt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, qr[m], acc[kt], 0, 0, 0);
+        acc[kt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, qr[m + 1], acc[kt], 0, 0, 0);
+        acc[kt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, qr[m + 2], acc[kt], 0, 0, 0);
+        acc[kt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, qr[m + 3], acc[kt], 0, 0, 0);
+      }
+    }
+  }
+  ATT_STAMP(2);
+
+  // softmax over the keys of query qi, in the accumulators
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+    if (kt < nkt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, acc[kt][r]);
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sm = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+    if (kt < nkt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        acc[kt][r] = exp2f(acc[kt][r] - mx);
+        sm += acc[kt][r];
+      }
+  sm += __shfl_xor(sm, 32, 64);
+  {
+    const float inv = __builtin_amdgcn_rcpf(sm);
+    const K3mDrop dr = k3m_drop_init(seed, p_drop);
+    const bool qok = qi < lq;
+    const long long prow = pbase + (long long)(qok ? qi : 0) * lk;
+    const bool vec = (lk & 3) == 0;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      if (kt < nkt) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          const int j0 = 32 * kt + 8 * a + 4 * kl;
+          float p4[4];
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int j = j0 + b;
+            p4[b] = acc[kt][4 * a + b] * inv;
+            acc[kt][4 * a + b] = j < lk ? p4[b] * k3m_drop(dr, off + prow + j) : 0.f;
+          }
+          if (qok) {
+            if (vec && j0 < lk) {
+              *reinterpret_cast<float4*>(probs + prow + j0) = make_float4(p4[0], p4[1], p4[2], p4[3]);
+            } else if (!vec) {
+#pragma unroll
+              for (int b = 0; b < 4; ++b)
+                if (j0 + b < lk) probs[prow + j0 + b] = p4[b];
+            }
+          }
+        }
+      }
+    }
+  }
+  ATT_STAMP(3);
+
+  // O^T = V^T P^T
+  floatx16 o[HD / 32];
+#pragma unroll
+  for (int dt = 0; dt < HD / 32; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+  const float* vbase = Vs + 4 * kl * HD + cl;
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) {
+    if (kt < nkt) {
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        const int key = 32 * kt + (st & 3) + 8 * (st >> 2);   // + 4 kl, in vbase
+#pragma unroll
+        for (int dt = 0; dt < HD / 32; ++dt)
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(vbase[key * HD + 32 * dt], acc[kt][st], o[dt], 0, 0, 0);
+      }
+    }
+  }
+  if (qi < lq) {
+    float* dst = ctx + (qrow0 + qi) * ldc + hoff + 4 * kl;
+#pragma unroll
+    for (int dt = 0; dt < HD / 32; ++dt)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        *reinterpret_cast<float4*>(dst + 32 * dt + 8 * a) =
+            make_float4(o[dt][4 * a], o[dt][4 * a + 1], o[dt][4 * a + 2], o[dt][4 * a + 3]);
+  }
+  ATT_STAMP(4);
+}
+
+size_t fwd_reg_lds(int lk, int hd) {
+  const size_t LK = (lk + 31) & ~31;
+  return sizeof(float) * (2 * LK * hd + LK);
+}
+
 size_t fwd_lds(int lq, int lk, int hd) {
   const size_t LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
   return sizeof(float) * (LQ * hd + LK * hd + LQ * LK);
@@ -533,6 +730,26 @@ void launch_bwd(const void* dctx, long long ldc, const void* o, long long ldo, c
 
 }  // namespace
 
+// the register-softmax forward serves fp32 heads whose K and V fit 2 workgroups per CU
+static const bool kAttnFwdReg = [] {
+  const char* e = std::getenv("K3M_ATTN_FWD_REG");
+  return !(e && e[0] == '0');
+}();
+
+template <int HD>
+void launch_fwd_reg(const void* q, long long ldq, const void* k, long long ldk, const void* v, long long ldv,
+                    const float* kmask, void* ctx, long long ldc, float* probs, int nseq, int lq, int lk, int nh,
+                    float scale, float p_drop, uint64_t seed, uint64_t off, hipStream_t st) {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)attn_fwd_reg_kernel<HD>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    done = true;
+  }
+  hipLaunchKernelGGL(attn_fwd_reg_kernel<HD>, dim3(nseq * nh), dim3(256), fwd_reg_lds(lk, HD), st, (const float*)q, ldq,
+                     (const float*)k, ldk, (const float*)v, ldv, kmask, (float*)ctx, ldc, probs, lq, lk, nh, scale, p_drop,
+                     seed, off);
+}
+
 extern "C" int k3m_attn_fwd(const void* q, long long ldq, const void* k, long long ldk, const void* v, long long ldv,
                             const float* kmask, void* ctx, long long ldc, float* probs, int nseq, int lq, int lk,
                             int nh, int hd, float scale, float p_drop, uint64_t seed, uint64_t off, int dtype,
@@ -545,6 +762,15 @@ extern "C" int k3m_attn_fwd(const void* q, long long ldq, const void* k, long lo
   const size_t lds = fwd_lds(lq, lk, hd);
   K3M_ARG(lds <= (size_t)LDS_MAX);
   const bool small = false;   // the forward gains nothing from the short build (measured)
+  const int LK = (lk + 31) & ~31;
+  if (dtype == K3M_F32 && kAttnFwdReg && (hd == 64 || hd == 96 || hd == 128) && LK * hd <= 8192 &&
+      vec_ok(ctx, ldc, dtype) && (reinterpret_cast<uintptr_t>(probs) & 15) == 0) {
+    if (hd == 64) launch_fwd_reg<64>(q, ldq, k, ldk, v, ldv, kmask, ctx, ldc, probs, nseq, lq, lk, nh, scale, p_drop, seed, off, st);
+    else if (hd == 96) launch_fwd_reg<96>(q, ldq, k, ldk, v, ldv, kmask, ctx, ldc, probs, nseq, lq, lk, nh, scale, p_drop, seed, off, st);
+    else launch_fwd_reg<128>(q, ldq, k, ldk, v, ldv, kmask, ctx, ldc, probs, nseq, lq, lk, nh, scale, p_drop, seed, off, st);
+    K3M_CHECK_LAUNCH();
+    return 0;
+  }
   if (dtype == K3M_F32) {
     if (small) launch_fwd<float, 64, 4>(q, ldq, k, ldk, v, ldv, kmask, ctx, ldc, probs, nseq, lq, lk, nh, hd, scale, p_drop, seed, off, lds, st);
     else launch_fwd<float, 128, 8>(q, ldq, k, ldk, v, ldv, kmask, ctx, ldc, probs, nseq, lq, lk, nh, hd, scale, p_drop, seed, off, lds, st);

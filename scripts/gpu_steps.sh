@@ -36,6 +36,7 @@ for s in "$@"; do
     apaths) step apaths 300 python scripts/attn_paths.py ;;
     dcost) step dcost 300 python scripts/dropout_cost.py ;;
     stamps) step stamps 120 scripts/lab/attn_stamps ;;
+    stamps0) K3M_ATTN_FWD_REG=0 step stamps0 120 scripts/lab/attn_stamps ;;
     pmcattn) step pmcattn 300 scripts/lab/pmc_attn.sh 0 att0 ;;
     tattn) step tattn 600 python -u -m pytest tests -m gpu -k "attn or attention" -x -q --timeout 300 --timeout-method thread ;;
     tbf) step tbf 600 python -m pytest tests/test_gpu_gemm_bf16.py -q ;;

@@ -57,6 +57,7 @@ int main(int argc, char** argv) {
   const int shapes[][5] = {{128, 128, 128, 12, 64}, {128, 36, 36, 12, 64}, {128, 37, 37, 8, 128},
                            {64, 128, 37, 8, 128},  {64, 37, 128, 8, 128}};
   const char* fn[] = {"stage_QK", "S", "V(w0)", "softmax", "PV"};
+  const char* fr[] = {"stage", "S(w0)", "softmax(w0)", "PV+store(w0)"};
   const char* bn[] = {"stage+D", "dS", "K+dQ", "Pd+dV", "Q+dK"};
   hipStream_t st;
   CK(hipStreamCreate(&st));
@@ -81,7 +82,10 @@ int main(int argc, char** argv) {
     for (int it = 0; it < 4; ++it)
       if (k3m_attn_fwd(q, D, k, D, v, D, mask, ctx, D, probs, nseq, lq, lk, nh, hd, sc, 0.1f, 1, 0, K3M_F32, st)) return 1;
     CK(hipStreamSynchronize(st));
-    report("fwd", nseq * nh, 6, fn);
+    const char* env = std::getenv("K3M_ATTN_FWD_REG");
+    const bool reg = !(env && env[0] == '0') && (hd == 64 || hd == 96 || hd == 128) && ((lk + 31) & ~31) * hd <= 8192;
+    if (reg) report("fwd(reg)", nseq * nh, 5, fr);
+    else report("fwd", nseq * nh, 6, fn);
     for (int it = 0; it < 4; ++it)
       if (k3m_attn_bwd(dctx, D, ctx, D, q, D, k, D, v, D, probs, dq, dk, dv, D, D, D, nseq, lq, lk, nh, hd, sc, 0.1f, 1,
                        0, K3M_F32, st))
