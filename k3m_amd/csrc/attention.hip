@@ -679,6 +679,262 @@ size_t fwd_reg_lds(int lk, int hd) {
   return sizeof(float) * (2 * LK * hd + LK);
 }
 
+// 16-byte global -> LDS copy (global_load_lds_dwordx4): the LDS destination is the wave-uniform base
+// plus 16 * lane
+__device__ __forceinline__ void glds16(const float* g, float* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+// ------------------------------------------------------------------ backward, keys on the lanes
+// fp32 partner of attn_fwd_reg_kernel (LQ*HD <= 8192).  Workgroup per (sequence, head), 4 waves:
+//   key phase   wave w owns keys 32w..32w+31 (on the MFMA lanes; V rows in registers):
+//               dPd = dO V^T (A = dO rows from a swizzled LDS image, 16-byte reads), then per element
+//               dS = P (dPd m - D), Pd = P m (P prefetched from the forward, m the regenerated dropout
+//               scale), both kept in accumulators; dV^T = dO^T Pd and dK^T = scale Q^T dS take them as
+//               B operands (k = query crow(s, kl)), A from LDS at per-step offsets; 16-byte stores
+//   dS image    written once to LDS (over dO / Q), then
+//   query phase wave w owns queries 32w..: dQ = scale dS K (A = dS rows, 16-byte reads; B = K rows).
+// D = rowsum(dO o O) from dot products of the staged 16-byte chunks.
+template <int HD>
+__global__ __launch_bounds__(256, 1) void attn_bwd_reg_kernel(
+    const float* __restrict__ dctx, long long ldc, const float* __restrict__ o, long long ldo,
+    const float* __restrict__ q, long long ldq, const float* __restrict__ k, long long ldk,
+    const float* __restrict__ v, long long ldv, const float* __restrict__ probs, float* __restrict__ dq,
+    float* __restrict__ dk, float* __restrict__ dv, long long lddq, long long lddk, long long lddv, int lq, int lk,
+    int nh, float scale, float p_drop, uint64_t seed, uint64_t off) {
+  constexpr int NTH = 256, HH = HD / 2, NCH = HD / 4;
+  constexpr int SWZ = (HD % 64 == 0) ? 15 : 7;
+  constexpr int UQ = 8192 / 4 / NTH;     // chunks per thread of a [LQ][HD] operand (LQ*HD <= 8192)
+  constexpr int UK = 128 * NCH / NTH;    // chunks per thread of K (LK <= 128)
+  extern __shared__ float smem[];
+  const int s = blockIdx.x / nh, h = blockIdx.x % nh;
+  const int LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
+  float* dOs = smem;              // [LQ][HD], chunk c of row i at chunk c ^ (i & SWZ)
+  float* Qs = dOs + LQ * HD;      // [LQ][HD]
+  float* Ks = Qs + LQ * HD;       // [LK][HD]
+  float* Ds = Ks + LK * HD;       // [LQ]
+  float* scr = Ds + LQ;           // [LQ][NCH] chunk dots of dO and O
+  float* dSs = smem;              // [LQ][LK] over dOs / Qs after the key phase, chunk c of row i at c ^ (i & sws)
+  const int sws = (LK % 64 == 0) ? 15 : 7;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
+  const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
+  const int hoff = h * HD;
+  const long long pbase = ((long long)s * nh + h) * lq * lk;
+  const K3mDrop dr = k3m_drop_init(seed, p_drop);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  ATT_STAMP(0);
+
+  {  // staging of dO (+ the D partials): every load first
+    float4 cdo[UQ], co[UQ];
+#pragma unroll
+    for (int u = 0; u < UQ; ++u) {
+      const int e = threadIdx.x + u * NTH, i = e / NCH, c = e % NCH;
+      const bool ok = e < LQ * NCH && i < lq;
+      const long long row = qrow0 + (ok ? i : 0);
+      cdo[u] = ok ? *reinterpret_cast<const float4*>(dctx + row * ldc + hoff + 4 * c) : z4;
+      co[u] = ok ? *reinterpret_cast<const float4*>(o + row * ldo + hoff + 4 * c) : z4;
+    }
+#pragma unroll
+    for (int u = 0; u < UQ; ++u) {
+      const int e = threadIdx.x + u * NTH, i = e / NCH, c = e % NCH;
+      if (e < LQ * NCH) {
+        *reinterpret_cast<float4*>(dOs + i * HD + 4 * (c ^ (i & SWZ))) = cdo[u];
+        scr[e] = cdo[u].x * co[u].x + cdo[u].y * co[u].y + cdo[u].z * co[u].z + cdo[u].w * co[u].w;
+      }
+    }
+  }
+  const int key = 32 * w + cl;      // this lane's key in the key phase
+  const bool kw = 32 * w < LK;      // wave-uniform
+  float vr[HH];                     // V[key][kl*HH + m]
+  {
+    const bool ok = kw && key < lk;
+    const float* src = v + (krow0 + (ok ? key : 0)) * ldv + hoff + kl * HH;
+#pragma unroll
+    for (int c = 0; c < HH / 4; ++c) {
+      const float4 t = ok ? *reinterpret_cast<const float4*>(src + 4 * c) : z4;
+      vr[4 * c] = t.x;
+      vr[4 * c + 1] = t.y;
+      vr[4 * c + 2] = t.z;
+      vr[4 * c + 3] = t.w;
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < LQ) {
+    float a = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) a += scr[threadIdx.x * NCH + c];
+    Ds[threadIdx.x] = a;
+  }
+  __syncthreads();
+  ATT_STAMP(1);
+  // Q and K are needed from the dV/dK phase on: global -> LDS copies (no registers) that fly during
+  // the dPd MFMAs.  A wave-instruction writes 64 consecutive 16-byte chunks (the plain row-major
+  // images); chunks of padding rows are zeroed with ordinary stores instead.
+#pragma unroll
+  for (int u = 0; u < UQ; ++u) {
+    const int e = threadIdx.x + u * NTH, i = e / NCH, c = e % NCH;
+    if (e < LQ * NCH) {   // wave-uniform (LQ*NCH is a multiple of 512)
+      if (i < lq) glds16(q + (qrow0 + i) * ldq + hoff + 4 * c, Qs + 4 * (u * NTH + 64 * w));
+      else *reinterpret_cast<float4*>(Qs + 4 * e) = z4;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < UK; ++u) {
+    const int e = threadIdx.x + u * NTH, j = e / NCH, c = e % NCH;
+    if (e < LK * NCH) {
+      if (j < lk) glds16(k + (krow0 + j) * ldk + hoff + 4 * c, Ks + 4 * (u * NTH + 64 * w));
+      else *reinterpret_cast<float4*>(Ks + 4 * e) = z4;
+    }
+  }
+
+  const int nqt = LQ >> 5;
+  floatx16 acc[4], pdv[4];   // rows: queries 32qt + crow(r, kl); lanes: keys
+  if (kw) {
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {   // the forward's probabilities, ahead of the MFMAs
+      if (qt < nqt) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qr = 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * kl;
+          pdv[qt][r] = (qr < lq && key < lk) ? probs[pbase + (long long)qr * lk + key] : 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {   // dPd = dO V^T
+      if (qt < nqt) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[qt][r] = 0.f;
+        const int ar = 32 * qt + cl;
+        const float* arow = dOs + ar * HD;
+        const int sw = ar & SWZ;
+#pragma unroll
+        for (int m = 0; m < HH; m += 4) {
+          const float4 a4 = *reinterpret_cast<const float4*>(arow + 4 * (((kl * HH + m) >> 2) ^ sw));
+          acc[qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, vr[m], acc[qt], 0, 0, 0);
+          acc[qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, vr[m + 1], acc[qt], 0, 0, 0);
+          acc[qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, vr[m + 2], acc[qt], 0, 0, 0);
+          acc[qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, vr[m + 3], acc[qt], 0, 0, 0);
+        }
+      }
+    }
+    ATT_STAMP(2);
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {   // dS, Pd
+      if (qt < nqt) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          const float4 d4 = *reinterpret_cast<const float4*>(Ds + 32 * qt + 8 * a + 4 * kl);
+          const float dd[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int r = 4 * a + b, qr = 32 * qt + 8 * a + 4 * kl + b;
+            const bool ok = qr < lq && key < lk;
+            const float m = k3m_drop(dr, off + pbase + (long long)(ok ? qr : 0) * lk + (ok ? key : 0));
+            const float p = pdv[qt][r];
+            acc[qt][r] = ok ? p * (acc[qt][r] * m - dd[b]) : 0.f;
+            pdv[qt][r] = p * m;
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();   // Q and K copies landed (the barrier waits for this wave's copies first)
+  if (kw) {
+    // dV^T = dO^T Pd, dK^T = Q^T dS (B operands from the accumulators)
+    floatx16 ov[HD / 32], ok_[HD / 32];
+#pragma unroll
+    for (int dt = 0; dt < HD / 32; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        ov[dt][r] = 0.f;
+        ok_[dt][r] = 0.f;
+      }
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      if (qt < nqt) {
+#pragma unroll
+        for (int st = 0; st < 16; ++st) {
+          const int row = 32 * qt + (st & 3) + 8 * (st >> 2) + 4 * kl;
+          const int sw = row & SWZ;
+#pragma unroll
+          for (int dt = 0; dt < HD / 32; ++dt) {
+            const int d = 32 * dt + cl;
+            const float a_do = dOs[row * HD + 4 * ((d >> 2) ^ sw) + (d & 3)];
+            const float a_q = Qs[row * HD + d];
+            ov[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_do, pdv[qt][st], ov[dt], 0, 0, 0);
+            ok_[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_q, acc[qt][st], ok_[dt], 0, 0, 0);
+          }
+        }
+      }
+    }
+    if (key < lk) {
+      float* pv = dv + (krow0 + key) * lddv + hoff + 4 * kl;
+      float* pk = dk + (krow0 + key) * lddk + hoff + 4 * kl;
+#pragma unroll
+      for (int dt = 0; dt < HD / 32; ++dt)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          *reinterpret_cast<float4*>(pv + 32 * dt + 8 * a) =
+              make_float4(ov[dt][4 * a], ov[dt][4 * a + 1], ov[dt][4 * a + 2], ov[dt][4 * a + 3]);
+          *reinterpret_cast<float4*>(pk + 32 * dt + 8 * a) =
+              make_float4(ok_[dt][4 * a] * scale, ok_[dt][4 * a + 1] * scale, ok_[dt][4 * a + 2] * scale,
+                          ok_[dt][4 * a + 3] * scale);
+        }
+    }
+  }
+  __syncthreads();   // every wave is done with dOs / Qs
+  ATT_STAMP(3);
+  if (kw) {
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt)
+      if (qt < nqt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qr = 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * kl;
+          dSs[qr * LK + 4 * ((key >> 2) ^ (qr & sws)) + (key & 3)] = acc[qt][r];
+        }
+  }
+  __syncthreads();
+  if (32 * w < LQ) {   // dQ = scale dS K for queries 32w..32w+31
+    floatx16 oq[HD / 32];
+#pragma unroll
+    for (int dt = 0; dt < HD / 32; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oq[dt][r] = 0.f;
+    const int ar = 32 * w + cl, LH = LK >> 1;
+    const float* arow = dSs + ar * LK;
+    const int sw = ar & sws;
+    const float* kb = Ks + kl * LH * HD + cl;
+    for (int m = 0; m < LH; m += 4) {
+      const float4 a4 = *reinterpret_cast<const float4*>(arow + 4 * (((kl * LH + m) >> 2) ^ sw));
+      const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int dt = 0; dt < HD / 32; ++dt)
+          oq[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], kb[(m + i) * HD + 32 * dt], oq[dt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qr = 32 * w + (r & 3) + 8 * (r >> 2) + 4 * kl;
+      if (qr < lq) {
+        float* dst = dq + (qrow0 + qr) * lddq + hoff + cl;
+#pragma unroll
+        for (int dt = 0; dt < HD / 32; ++dt) dst[32 * dt] = oq[dt][r] * scale;
+      }
+    }
+  }
+  ATT_STAMP_END(4);
+}
+
+size_t bwd_reg_lds(int lq, int lk, int hd) {
+  const size_t LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
+  return sizeof(float) * (2 * LQ * hd + LK * hd + LQ + LQ * (hd / 4));
+}
+
 size_t fwd_lds(int lq, int lk, int hd) {
   const size_t LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
   return sizeof(float) * (LQ * hd + LK * hd + LQ * LK);
@@ -782,6 +1038,27 @@ extern "C" int k3m_attn_fwd(const void* q, long long ldq, const void* k, long lo
   return 0;
 }
 
+static const bool kAttnBwdReg = [] {
+  const char* e = std::getenv("K3M_ATTN_BWD_REG");
+  return !(e && e[0] == '0');
+}();
+
+template <int HD>
+void launch_bwd_reg(const void* dctx, long long ldc, const void* o, long long ldo, const void* q, long long ldq,
+                    const void* k, long long ldk, const void* v, long long ldv, const float* probs, void* dq, void* dk,
+                    void* dv, long long lddq, long long lddk, long long lddv, int nseq, int lq, int lk, int nh,
+                    float scale, float p_drop, uint64_t seed, uint64_t off, hipStream_t st) {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)attn_bwd_reg_kernel<HD>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    done = true;
+  }
+  hipLaunchKernelGGL(attn_bwd_reg_kernel<HD>, dim3(nseq * nh), dim3(256), bwd_reg_lds(lq, lk, HD), st,
+                     (const float*)dctx, ldc, (const float*)o, ldo, (const float*)q, ldq, (const float*)k, ldk,
+                     (const float*)v, ldv, probs, (float*)dq, (float*)dk, (float*)dv, lddq, lddk, lddv, lq, lk, nh, scale,
+                     p_drop, seed, off);
+}
+
 extern "C" int k3m_attn_bwd(const void* dctx, long long ldc, const void* o, long long ldo, const void* q, long long ldq,
                             const void* k, long long ldk, const void* v, long long ldv, const float* probs, void* dq,
                             void* dk, void* dv, long long lddq, long long lddk, long long lddv, int nseq, int lq, int lk,
@@ -795,6 +1072,17 @@ extern "C" int k3m_attn_bwd(const void* dctx, long long ldc, const void* o, long
   const size_t lds = bwd_lds(lq, lk, hd);
   K3M_ARG(lds <= (size_t)LDS_MAX);
   const bool small = lq <= 64 && lk <= 64 && hd <= 64;   // d = 128 runs better as one 8-wave block
+  const int LQ = (lq + 31) & ~31;
+  // (for LK <= 64 the 64-row LDS kernel is faster: three workgroups per CU against one)
+  if (dtype == K3M_F32 && kAttnBwdReg && (hd == 64 || hd == 96 || hd == 128) && LQ * hd <= 8192 && lk > 64 &&
+      bwd_reg_lds(lq, lk, hd) <= (size_t)LDS_MAX && vec_ok(o, ldo, dtype) && vec_ok(dk, lddk, dtype) &&
+      vec_ok(dv, lddv, dtype)) {
+    if (hd == 64) launch_bwd_reg<64>(dctx, ldc, o, ldo, q, ldq, k, ldk, v, ldv, probs, dq, dk, dv, lddq, lddk, lddv, nseq, lq, lk, nh, scale, p_drop, seed, off, st);
+    else if (hd == 96) launch_bwd_reg<96>(dctx, ldc, o, ldo, q, ldq, k, ldk, v, ldv, probs, dq, dk, dv, lddq, lddk, lddv, nseq, lq, lk, nh, scale, p_drop, seed, off, st);
+    else launch_bwd_reg<128>(dctx, ldc, o, ldo, q, ldq, k, ldk, v, ldv, probs, dq, dk, dv, lddq, lddk, lddv, nseq, lq, lk, nh, scale, p_drop, seed, off, st);
+    K3M_CHECK_LAUNCH();
+    return 0;
+  }
   if (dtype == K3M_F32) {
     if (small) launch_bwd<float, 64, 4>(dctx, ldc, o, ldo, q, ldq, k, ldk, v, ldv, probs, dq, dk, dv, lddq, lddk, lddv, nseq, lq, lk, nh, hd, scale, p_drop, seed, off, lds, st);
     else launch_bwd<float, 128, 8>(dctx, ldc, o, ldo, q, ldq, k, ldk, v, ldv, probs, dq, dk, dv, lddq, lddk, lddv, nseq, lq, lk, nh, hd, scale, p_drop, seed, off, lds, st);

@@ -58,6 +58,7 @@ int main(int argc, char** argv) {
                            {64, 128, 37, 8, 128},  {64, 37, 128, 8, 128}};
   const char* fn[] = {"stage_QK", "S", "V(w0)", "softmax", "PV"};
   const char* fr[] = {"stage", "S(w0)", "softmax(w0)", "PV+store(w0)"};
+  const char* br[] = {"stage+D", "dPd(w0)", "dS,dV,dK", "dS image+dQ"};
   const char* bn[] = {"stage+D", "dS", "K+dQ", "Pd+dV", "Q+dK"};
   hipStream_t st;
   CK(hipStreamCreate(&st));
@@ -91,7 +92,10 @@ int main(int argc, char** argv) {
                        0, K3M_F32, st))
         return 1;
     CK(hipStreamSynchronize(st));
-    report("bwd", nseq * nh, 6, bn);
+    const char* envb = std::getenv("K3M_ATTN_BWD_REG");
+    const bool regb = !(envb && envb[0] == '0') && (hd == 64 || hd == 96 || hd == 128) && ((lq + 31) & ~31) * hd <= 8192 && lk > 64;
+    if (regb) report("bwd(reg)", nseq * nh, 5, br);
+    else report("bwd", nseq * nh, 6, bn);
     for (float* p : {q, k, v, dctx, mask, ctx, probs, dq, dk, dv}) CK(hipFree(p));
   }
   return 0;
