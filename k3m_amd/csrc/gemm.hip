@@ -2,8 +2,10 @@
 //
 // fp32 operands, default (K3M_F32_SPLIT_BF16X6): the bf16x6 split kernel of gemm_x6_tile.h on the
 // bf16 matrix cores (fp32 accuracy, 2.67x the f32-MFMA roofline), tile chosen per shape:
-//   * 256x128x32 (8 waves, 1 block/CU, 144 KB LDS) for the large GEMMs and the split-K weight
-//     gradients (ops._splitk sizes the split to whole waves of 256 blocks);
+//   * 256x256x16 (8 waves, 1 block/CU, 96 KB LDS) for the large GEMMs and the split-K weight
+//     gradients when its half-as-many blocks do not cost an extra wave (prefer_256x256);
+//   * 256x128x32 (8 waves, 1 block/CU, 144 KB LDS) otherwise (ops._splitk sizes the split to whole
+//     waves of 256 of these blocks);
 //   * 128x128x32 (4 waves) for mid-size grids;
 //   * 64x64x16 for the small co-attention GEMMs.
 // K3M_F32_MFMA_F32 (and unaligned operands): the v_mfma_f32_32x32x2_f32 kernel of gemm_f32_tile.h
@@ -110,6 +112,15 @@ long long nblocks(const K3mGemm& g, int bm, int bn) {
   return (long long)((g.m + bm - 1) / bm) * ((g.n + bn - 1) / bn) * (g.splitk > 1 ? g.splitk : 1);
 }
 
+// 256x256x16 vs 256x128x32 x6 tiles: the larger tile halves the split VALU and the LDS fragment
+// reads per MFMA and ran 7-11 % faster per block-wave on the K3M shapes (scripts/lab,
+// profiles/r1_gemm_lab_x6_v4.txt), but has half the blocks: take it unless it costs a whole extra wave
+// of 256 blocks (the 8,192-row co-attention FFN: 384 blocks = 1.5 waves vs 768 = 3).
+bool prefer_256x256(const K3mGemm& g) {
+  const long long w128 = (nblocks(g, 256, 128) + 255) / 256, w256 = (nblocks(g, 256, 256) + 255) / 256;
+  return 2.0 * (double)w256 / 1.08 < (double)w128;
+}
+
 }  // namespace
 
 int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st);  // gemm_bf16.hip
@@ -136,7 +147,18 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
   // (2,304-8,192 rows) otherwise leave CUs idle
   int rc;
   if (vec && g.f32_algo == K3M_F32_SPLIT_BF16X6) {
-    if (g.splitk > 1 || nblocks(g, 256, 128) >= 200) rc = launch_x6<256, 128, 4, 2, 32, 1>(g, ak, bk, st);
+    if (g.splitk > 1 || nblocks(g, 256, 128) >= 200) {
+      if ((ak || !bk) && prefer_256x256(g)) {
+        // wave layout per operand layout (scripts/lab, best of passes): 4x2 for the forward (both
+        // K-contiguous), 2x4 when B is MN-contiguous (dgrad, and the single-register-set loop for
+        // the weight gradients)
+        if (ak && bk) rc = launch_x6_epi<256, 256, 4, 2, 16, 1, true, true>(g, st);
+        else if (ak) rc = launch_x6_epi<256, 256, 2, 4, 16, 1, true, false>(g, st);
+        else rc = launch_x6_epi<256, 256, 2, 4, 16, 1, false, false, false>(g, st);
+      } else {
+        rc = launch_x6<256, 128, 4, 2, 32, 1>(g, ak, bk, st);
+      }
+    }
     else if (nblocks(g, 128, 128) >= 200) rc = launch_x6<128, 128, 2, 2, 32, 1>(g, ak, bk, st);
     // 64x64 runs at BK = 16: the BK = 32 build of this tile (ROCm 7.2 hipcc) returned C = alpha*AB
     // without the beta*C term for scattered 16-lane groups (scripts/lab/gemm_dbg.hip reproduces it;

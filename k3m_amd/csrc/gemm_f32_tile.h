@@ -118,10 +118,10 @@ __device__ __forceinline__ int xcd_remap(int id, int nblk) {
 
 // Block-tile coordinates: XCD remap, then GROUP rows of tiles walk N together (L2 reuse of the
 // A panel inside one XCD).
+template <int GROUP = 8>
 __device__ __forceinline__ void tile_coords(int M, int N, int TBM, int TBN, int& m0, int& n0) {
   const int tm = (M + TBM - 1) / TBM, tn = (N + TBN - 1) / TBN;
   const int id = xcd_remap(blockIdx.x, tm * tn);
-  constexpr int GROUP = 8;
   const int group_sz = GROUP * tn;
   const int first_m = (id / group_sz) * GROUP;
   const int gm_sz = min(tm - first_m, GROUP);

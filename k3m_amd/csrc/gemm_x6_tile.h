@@ -379,7 +379,8 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm_x6_kernel(K3mGemm g) {
   constexpr int WORDS = (LDS_BF16 / 2 > EPI_F32 ? LDS_BF16 / 2 : EPI_F32);
   __shared__ __attribute__((aligned(16))) float smem[WORDS];
   int m0, n0;
-  K3M_F32_NS::tile_coords(g.m, g.n, TBM, TBN, m0, n0);
+  // VAR bits 16 / 32 (lab): 4 / 2 row-tiles per N walk instead of 8
+  K3M_F32_NS::tile_coords<(VAR & 16) ? 4 : (VAR & 32) ? 2 : 8>(g.m, g.n, TBM, TBN, m0, n0);
   int kbeg = 0, kend = g.k;
   if (g.splitk > 1) {
     const int per = ((g.k + g.splitk - 1) / g.splitk + BK - 1) / BK * BK;

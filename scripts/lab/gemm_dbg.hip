@@ -32,7 +32,7 @@ void launch(const K3mGemm& g, hipStream_t st) {
 
 __global__ void visit_kernel(int M, int N, int TBM, int TBN, int* visits) {
   int m0, n0;
-  lab_f32::tile_coords(M, N, TBM, TBN, m0, n0);
+  lab_f32::tile_coords<>(M, N, TBM, TBN, m0, n0);
   if (threadIdx.x == 0) atomicAdd(&visits[(m0 / TBM) * ((N + TBN - 1) / TBN) + n0 / TBN], 1);
 }
 

@@ -81,16 +81,10 @@ std::vector<std::pair<std::string, Launcher>> variants() {
   return {
       {"shipped in loop", launch_shipped},
       {"x6 256x128 4x2 bk32", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_>},
-      {"x6 256x128 bk32 v2 prio", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, true, 2>},
-      {"x6 256x128 bk32 v3 loadpin+prio", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, true, 3>},
-      {"x6 256x128 bk32 v6 prio+storepin", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, true, 6>},
-      {"x6 256x128 bk32 v7 all", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, true, 7>},
-      {"x6 256x128 bk32 v8 prio-first", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, true, 8>},
-      {"x6 256x128 bk32 v12 prio-first+storepin", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, true, 12>},
-      {"x6 256x128 bk32 nopipe v2", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, false, 2>},
-      {"x6 256x128 bk32 nopipe v8", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, false, 8>},
-      {"x6 256x128 bk16 2blk nopipe v8", launch_x6<256, 128, 4, 2, 16, 4, EPI, AK, BK_, false, 8>},
       {"x6 256x128 bk32 nopipe", launch_x6<256, 128, 4, 2, 32, 1, EPI, AK, BK_, false>},
+      {"x6 256x256 2x4 bk16", launch_x6<256, 256, 2, 4, 16, 1, EPI, AK, BK_>},
+      {"x6 256x256 2x4 bk16 nopipe", launch_x6<256, 256, 2, 4, 16, 1, EPI, AK, BK_, false>},
+      {"x6 256x256 4x2 bk16", launch_x6<256, 256, 4, 2, 16, 1, EPI, AK, BK_>},
   };
 }
 

@@ -48,6 +48,8 @@ def _case(dev, m, n, k, at, bt, splitk=1, seed=0):
 
 
 @pytest.mark.parametrize("m,n,k", [(4096, 3072, 768),   # 256x256x16 tiles
+                                   (4000, 3000, 772),   # 256x256x16, ragged M/N and a partial k-tile
+                                   (20992, 768, 768),   # 256x256x16: one wave of 246 blocks instead of two of 256x128
                                    (2304, 2304, 768),   # 128x128x32 tiles
                                    (1024, 1024, 2048),  # 64x64x32 tiles
                                    (300, 200, 100)])    # ragged edges
@@ -59,6 +61,12 @@ def test_x6_accuracy_vs_fp64(dev, m, n, k, at, bt):
 @pytest.mark.parametrize("splitk", [3, 5])
 def test_x6_splitk_accuracy(dev, splitk):
     _case(dev, 768, 1024, 20000, 1, 0, splitk=splitk)
+
+
+@pytest.mark.parametrize("at,bt", [(1, 0), (0, 0), (0, 1)])
+def test_x6_splitk_256x256(dev, at, bt):
+    # the weight-gradient shape (3072 x 768 over 20k rows, split 7) runs on 256x256x16 tiles
+    _case(dev, 3072, 768, 20000, at, bt, splitk=7)
 
 
 def test_x6_epilogues_match_torch(dev):
@@ -79,10 +87,11 @@ def test_x6_epilogues_match_torch(dev):
     assert float((dx - xr.grad).abs().max()) < 2e-5 * float(xr.grad.abs().max())
 
 
-@pytest.mark.parametrize("m,n,k", [(4096, 3072, 768), (2304, 2304, 768), (1000, 3072, 768), (1024, 1024, 2048)])
-@pytest.mark.parametrize("at,bt", [(0, 1), (0, 0), (1, 0)])
+@pytest.mark.parametrize("m,n,k", [(4096, 3072, 768), (4000, 3000, 772), (20992, 768, 768), (8192, 3072, 768),
+                                   (2304, 2304, 768), (1000, 3072, 768), (1024, 1024, 2048)])
+@pytest.mark.parametrize("at,bt", [(0, 1), (0, 0), (1, 0), (1, 1)])
 def test_x6_beta_all_tiles(dev, m, n, k, at, bt):
-    """C = alpha*op(A)op(B) + beta*C on every x6 tile path (256x128, 128x128, 64x64), repeated: the
+    """C = alpha*op(A)op(B) + beta*C on every x6 tile path (256x256, 256x128, 128x128, 64x64), repeated: the
     read-modify-write of C must see the old value in every lane (regression for a 64x64 BK=32 build)."""
     from k3m_amd import ops, _lib as L
     g = torch.Generator(device="cpu").manual_seed(m * 7 + n + k)
