@@ -18,6 +18,8 @@
 // applies alpha/beta.  bf16 operands go to gemm_bf16.hip.
 #include "gemm_x6_tile.h"
 
+#include <cstdlib>
+
 namespace {
 
 using k3m_f32::gemm_f32_kernel;
@@ -116,7 +118,17 @@ long long nblocks(const K3mGemm& g, int bm, int bn) {
 // reads per MFMA and ran 7-11 % faster per block-wave on the K3M shapes (scripts/lab,
 // profiles/r1_gemm_lab_x6_v4.txt), but has half the blocks: take it unless it costs a whole extra wave
 // of 256 blocks (the 8,192-row co-attention FFN: 384 blocks = 1.5 waves vs 768 = 3).
+// K3M_X6_TILE256 (bitmask, default 15): 1 forward (both K-contiguous), 2 dgrad (B MN-contiguous),
+// 4 weight gradients (both MN-contiguous), 8 the grouped launch; 0 keeps every GEMM on 256x128.
+const int kTile256 = [] {
+  const char* e = std::getenv("K3M_X6_TILE256");
+  return e ? std::atoi(e) : 15;
+}();
+
+int tile256_class(bool ak, bool bk) { return ak && bk ? 1 : ak ? 2 : !bk ? 4 : 0; }
+
 bool prefer_256x256(const K3mGemm& g) {
+  if (!(kTile256 & tile256_class(g.a_trans == 0, g.b_trans == 1))) return false;
   const long long w128 = (nblocks(g, 256, 128) + 255) / 256, w256 = (nblocks(g, 256, 256) + 255) / 256;
   return 2.0 * (double)w256 / 1.08 < (double)w128;
 }
@@ -183,13 +195,13 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
 // ------------------------------------------------------------------ grouped launch
 namespace {
 
-template <bool AK, bool BK_, bool PIPE>
+template <int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool PIPE>
 int launch_grouped_epi(const k3m_x6::GemmGroup& grp, int epi, hipStream_t st) {
   const dim3 grid(grp.start[grp.count]);
   switch (epi) {
 #define K3M_GROUP_CASE(E)                                                                                          \
     case E:                                                                                                        \
-      hipLaunchKernelGGL((k3m_x6::gemm_x6_grouped_kernel<256, 128, 4, 2, 32, AK, BK_, true, E, 1, PIPE>), grid,       \
+      hipLaunchKernelGGL((k3m_x6::gemm_x6_grouped_kernel<256, TBN, WM, WN, BK, AK, BK_, true, E, 1, PIPE>), grid,     \
                          dim3(512), 0, st, grp);                                                                   \
       break;
     K3M_GROUP_CASE(K3M_EPI_NONE)
@@ -213,6 +225,7 @@ extern "C" int k3m_gemm_grouped(const K3mGemm* gs, int count, hipStream_t st) {
   bool same = g0.dtype == K3M_F32 && g0.c_dtype == K3M_F32 && g0.f32_algo == K3M_F32_SPLIT_BF16X6;
   k3m_x6::GemmGroup grp = {};
   int nb = 0, live = 0;
+  long long nb128 = 0, nb256 = 0;
   for (int i = 0; i < count && same; ++i) {
     const K3mGemm& g = gs[i];
     same = g.a_trans == g0.a_trans && g.b_trans == g0.b_trans && g.epilogue == g0.epilogue && g.dtype == g0.dtype &&
@@ -222,8 +235,8 @@ extern "C" int k3m_gemm_grouped(const K3mGemm* gs, int count, hipStream_t st) {
            (g.ldb % 4 == 0) && ((bk ? g.k : g.n) % 4 == 0);
     if (g.m == 0 || g.n == 0) continue;
     grp.g[live] = g;
-    grp.start[live] = nb;
-    nb += (int)nblocks(g, 256, 128);
+    nb128 += nblocks(g, 256, 128);
+    nb256 += nblocks(g, 256, 256);
     ++live;
   }
   if (!same) {   // not one template: launch each on its own
@@ -241,14 +254,25 @@ extern "C" int k3m_gemm_grouped(const K3mGemm* gs, int count, hipStream_t st) {
     K3M_ARG((g.epilogue != K3M_EPI_BIAS_GELU && g.epilogue != K3M_EPI_DGELU) || g.aux);
   }
   if (live == 0) return 0;
+  const bool ak = g0.a_trans == 0, bk = g0.b_trans == 1;
+  // same tile rule as k3m_gemm, over the whole grid (prefer_256x256)
+  const long long w128 = (nb128 + 255) / 256, w256 = (nb256 + 255) / 256;
+  const bool t256 = (kTile256 & 8) && (kTile256 & tile256_class(ak, bk)) && 2.0 * (double)w256 / 1.08 < (double)w128;
+  for (int i = 0; i < live; ++i) {
+    grp.start[i] = nb;
+    nb += (int)nblocks(grp.g[i], 256, t256 ? 256 : 128);
+  }
   grp.start[live] = nb;
   grp.count = live;
-  const bool ak = g0.a_trans == 0, bk = g0.b_trans == 1;
   int rc;
-  if (ak && bk) rc = launch_grouped_epi<true, true, true>(grp, g0.epilogue, st);
-  else if (ak) rc = launch_grouped_epi<true, false, true>(grp, g0.epilogue, st);
-  else if (bk) rc = launch_grouped_epi<false, true, true>(grp, g0.epilogue, st);
-  else rc = launch_grouped_epi<false, false, false>(grp, g0.epilogue, st);
+  if (t256) {
+    if (ak && bk) rc = launch_grouped_epi<256, 4, 2, 16, true, true, true>(grp, g0.epilogue, st);
+    else if (ak) rc = launch_grouped_epi<256, 2, 4, 16, true, false, true>(grp, g0.epilogue, st);
+    else rc = launch_grouped_epi<256, 2, 4, 16, false, false, false>(grp, g0.epilogue, st);
+  } else if (ak && bk) rc = launch_grouped_epi<128, 4, 2, 32, true, true, true>(grp, g0.epilogue, st);
+  else if (ak) rc = launch_grouped_epi<128, 4, 2, 32, true, false, true>(grp, g0.epilogue, st);
+  else if (bk) rc = launch_grouped_epi<128, 4, 2, 32, false, true, true>(grp, g0.epilogue, st);
+  else rc = launch_grouped_epi<128, 4, 2, 32, false, false, false>(grp, g0.epilogue, st);
   if (rc) return rc;
   K3M_CHECK_LAUNCH();
   for (int i = 0; i < live; ++i) {
