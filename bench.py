@@ -1,25 +1,37 @@
 """Benchmark: K3M tri-modal pretraining step (bert_base_6layer_6conect) on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 64] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config {2,3,4,5}] [--dtype fp32|bf16]
+                    [--batch B] [--no-cpu-baseline]
 
 One step = forward + backward + (RCCL gradient all-reduce when N > 1) + AdamW + LR schedule over
-one synthetic batch resident in HBM (SURVEY.md §8(d) input spec; random token ids, 36x2048 region
-features, 10 PV triples).  N > 1: launched by torch.distributed.run, one rank per GPU, each rank
-processes its own bs=64 batch (weak scaling, global batch = 64 N).
+one synthetic batch resident in HBM (SURVEY.md §8(d) input spec: random token ids, region
+features, PV triples).  Workloads (BASELINE.json configs):
+  2 (default) bert_base_6layer_6conect fp32, bs=64/GPU, T=36, P=128, 36 boxes, 10 triples — the metric's config;
+  3 the same in bf16 (mixed precision: bf16 encoder, fp32 master weights / heads / optimizer);
+  4 T=128, 100 boxes, bs=256/GPU (bf16);   5 P=320, 50 triples (NPV 50), bs=128/GPU (bf16).
+N > 1: one rank per GPU over RCCL.  Under torch.distributed.run (WORLD_SIZE set) this process is a
+rank; with ``--gpus N`` and no WORLD_SIZE it launches ``torch.distributed.run --nproc-per-node N``
+itself, before touching the GPU, and exits with its status.  Each rank runs its own bs=B batch
+(weak scaling, global batch = B N); the timed region is bracketed by barrier + synchronize and the
+max over ranks is taken.
 
-Prints ONE JSON line (rank 0) with the driver's contract plus
-  roofline     — the dominant kernel (the fp32 MFMA GEMM of the text-layer FFN, timed with HIP
-                 events on its stream over the timed steps) against the f32 MFMA peak;
-  cpu_baseline — the CPU oracle (plain PyTorch fp32 restatement of the same step, oracle/) timed
-                 on the host cores on a bounded sample (rank 0, N = 1 only).
+Rank 0 prints ONE JSON line with the driver's contract plus
+  roofline        — the dominant kernel (the text-layer FFN1 GEMM, 2BT+2BP rows x 3072 x 768),
+                    timed with HIP events on its stream over the timed steps, against the peak of the
+                    arithmetic it runs on (fp32: bf16x6 split = bf16 dense peak / 6; bf16: bf16 peak);
+  coattn          — the co-attention blocks (18 layers: both directions' attention, projections,
+                    FFNs, LayerNorms; forward + backward) timed with HIP events: their algorithmic
+                    FLOPs / time against the same peak (north-star target >= 0.40);
+  cpu_baseline    — the CPU oracle (plain PyTorch fp32 restatement of the same step, oracle/) on the
+                    host cores, bounded sample (rank 0, N = 1 only).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
@@ -27,7 +39,32 @@ sys.path.insert(0, HERE)
 PEAK_F32_MFMA = 157.3e12      # MI355X f32 MFMA dense peak (MI355X_MICROARCH.md)
 PEAK_BF16_MFMA = 2.5e15
 PEAK_F32_X6 = PEAK_BF16_MFMA / 6   # fp32 GEMM as 6 bf16 MFMA partial products (gemm_x6_tile.h)
-REF_FLOPS_PER_SAMPLE = 319.31e9   # reference algorithmic fwd+bwd FLOPs/sample at config 2
+
+# BASELINE.json configs -> synthetic workload shapes
+CONFIGS = {
+    2: dict(B=64, T=36, P=128, nbox=36, n_triples=10, npv=20, dtype="fp32"),
+    3: dict(B=64, T=36, P=128, nbox=36, n_triples=10, npv=20, dtype="bf16"),
+    4: dict(B=256, T=128, P=128, nbox=100, n_triples=10, npv=20, dtype="bf16"),
+    5: dict(B=128, T=36, P=320, nbox=36, n_triples=50, npv=50, dtype="bf16"),
+}
+
+
+def ref_fwd_flops(T, P, R, Nt, H=768, I=3072, V=21128, Hv=1024, Iv=1024, Hb=1024, Cv=1601):
+    """Reference algorithmic forward FLOPs per sample (SURVEY.md §8(d) formula; 106.48 GF at config 2)."""
+    def f_t(L): return 2 * L * (4 * H * H + 2 * H * I) + 4 * L * L * H
+    def f_v(R_): return 2 * R_ * (4 * Hv * Hv + 2 * Hv * Iv) + 4 * R_ * R_ * Hv
+    c = coattn_fwd_flops(T, P, R, H, I, Hv, Iv, Hb)
+    return (24 * f_t(T) + 24 * f_t(P) + 12 * f_v(R) + c + 2 * R * (2048 + 5) * Hv
+            + 2 * (T + P) * (H * H + H * V) + 2 * R * (Hv * Hv + Hv * Cv)
+            + 3 * 2 * R * 3 * Hb * Hb + 3 * 2 * (T + P) * 3 * H * H + 2 * Nt * 3 * H * H)
+
+
+def coattn_fwd_flops(T, P, R, H=768, I=3072, Hv=1024, Iv=1024, Hb=1024):
+    """6 x c_layer(T,R) + 6 x c_layer_pv_v(P,R) + 6 x c_layer_pv_t(T,P) forward FLOPs per sample."""
+    def c_tv(L, R_): return (2 * R_ * (3 * Hv * Hb + Hb * Hv + 2 * Hv * Iv) + 2 * L * (3 * H * Hb + Hb * H + 2 * H * I)
+                             + 8 * L * R_ * Hb)
+    def c_tt(T_, P_): return (T_ + P_) * (2 * (3 * H * H + H * H + 2 * H * I)) + 8 * T_ * P_ * H
+    return 6 * c_tv(T, R) + 6 * c_tv(P, R) + 6 * c_tt(T, P)
 
 
 def parse():
@@ -35,15 +72,34 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--batch", type=int, default=64)
-    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
-                    help="fp32: configs[1] (the metric's config); bf16: mixed-precision encoder (configs[2])")
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
+    ap.add_argument("--dtype", default=None, choices=["fp32", "bf16"], help="default: the config's")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=2)
-    ap.add_argument("--cpu-steps", type=int, default=10)
+    ap.add_argument("--cpu-batch", type=int, default=8)
+    ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL) for real runs; gloo only to rehearse the "
                     "multi-rank path with several ranks sharing one GPU")
+    ap.add_argument("--master-port", type=int, default=0)
     return ap.parse_args()
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args):
+    """--gpus N without a torch.distributed.run parent: start N ranks as children (no GPU touched here)."""
+    port = args.master_port or free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 class GemmProbe(object):
@@ -55,6 +111,7 @@ class GemmProbe(object):
         self.active = False
 
     def install(self):
+        import torch
         from k3m_amd import ops
         orig = ops.gemm
         probe = self
@@ -77,37 +134,85 @@ class GemmProbe(object):
         return sum(s.elapsed_time(e) for s, e in self.events) / len(self.events)
 
 
+class CoattnProbe(object):
+    """HIP events around every co-attention block (the engine's lock-step runs of the three
+    co-attention layers of one schedule step, forward and backward)."""
+
+    def __init__(self):
+        self.events = []
+        self.active = False
+
+    def install(self):
+        import torch
+        from k3m_amd import engine
+        orig = engine._lockstep
+        probe = self
+
+        def wrapped(gens):
+            if not probe.active:
+                return orig(gens)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            r = orig(gens)
+            e.record()
+            probe.events.append((s, e))
+            return r
+
+        engine._lockstep = wrapped
+
+    def total_ms(self):
+        return sum(s.elapsed_time(e) for s, e in self.events)
+
+
 def pmc_traffic(key, kernel_prefix):
-    """HBM-side bytes per launch of the probed GEMM, from the committed rocprofv3 PMC passes
-    (profiles/r1_gemm_ffn1_pmc.json: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), or None."""
-    path = os.path.join(HERE, "profiles", "r1_gemm_ffn1_pmc.json")
+    """HBM-side bytes per launch of the probed GEMM from a committed rocprofv3 PMC record
+    (profiles/*_gemm_ffn1_pmc.json: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(HERE, "profiles", "*_gemm_ffn1_pmc.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if tuple(d.get("shape", ())) == tuple(key) and kernel_prefix in d.get("kernel", ""):
+            return int(d["traffic_bytes"]), os.path.relpath(path, HERE)
+    return None, None
+
+
+def cpu_model():
     try:
-        with open(path) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
-        return None
-    if tuple(d.get("shape", ())) != tuple(key) or kernel_prefix not in d.get("kernel", ""):
-        return None
-    return int(d["traffic_bytes"])
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
-def cpu_baseline(cfg, bsz, steps):
-    """Oracle (torch CPU fp32) fwd+bwd+AdamW on a bounded sample; baseline only."""
+def cpu_baseline(cfg, shape, bsz, steps):
+    """Oracle (torch CPU fp32) fwd+bwd+AdamW on a bounded sample of the same workload; baseline only."""
+    import torch
     from oracle import k3m_oracle as O
     from k3m_amd.weights import init_values
     from k3m_amd.synthetic import synthetic_batch, synthetic_noise
     ncores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
     torch.set_num_threads(ncores)
     P = {k: torch.from_numpy(v).requires_grad_(True) for k, v in init_values(cfg, 0).items()}
-    batch = synthetic_batch(cfg, bsz, "cpu", seed=99)
-    noise = synthetic_noise(cfg, bsz, seed=1)
+    T, Pl, nbox = shape["T"], shape["P"], shape["nbox"]
+    batch = synthetic_batch(cfg, bsz, "cpu", seed=99, T=T, P=Pl, n_boxes=nbox, n_triples=shape["n_triples"],
+                            npv=shape["npv"])
+    noise = synthetic_noise(cfg, bsz, seed=1, T=T, P=Pl, R=nbox + 1)
     NPV = batch["index_p"].shape[1]
+    nt = shape["n_triples"]
     ent = torch.full((bsz, NPV, 2), -1, dtype=torch.int64)
     val = torch.full((bsz, NPV, 2), -1, dtype=torch.int64)
     for i in range(bsz):
-        for j in range(10):
+        for j in range(nt):
             ent[i, j, 0] = (i + 1) % bsz if bsz > 1 else -1
-            val[i, j, 0] = (j + 1) % 10
+            ent[i, j, 1] = (i + 2) % bsz if bsz > 2 else -1
+            val[i, j, 0] = (j + 1) % nt
+            val[i, j, 1] = (j + 2) % nt
     state = {k: (torch.zeros_like(v), torch.zeros_like(v)) for k, v in P.items()}
 
     def step(t):
@@ -127,19 +232,28 @@ def cpu_baseline(cfg, bsz, steps):
         step(t + 2)
     dt = time.perf_counter() - t0
     return {"value": round(bsz * steps / dt, 4), "unit": "samples/s", "cores": ncores, "kind": "port",
-            "sample": "oracle/k3m_oracle.py fwd+bwd+AdamW, fp32, bs=%d, %d timed steps after 1 warm-up, "
-                      "%.1f s" % (bsz, steps, dt)}
+            "cpu_model": cpu_model(),
+            "sample": "oracle/k3m_oracle.py fwd+bwd+AdamW, fp32, bs=%d, %d timed steps after 1 warm-up, %.1f s "
+                      "(same shapes as the GPU workload; torch CPU, %d threads)" % (bsz, steps, dt, ncores)}
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.gpus != world:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    ddp = None
+    shape = dict(CONFIGS[args.config])
+    dtype = args.dtype or shape["dtype"]
+    B = args.batch or shape["B"]
+    dist = None
     if world > 1:
         import torch.distributed as dist
         if args.backend == "nccl":
@@ -150,40 +264,46 @@ def main():
     from k3m_amd.config import pretrain_config
     from k3m_amd.trainer import Trainer
     from k3m_amd.synthetic import synthetic_batch
+    from k3m_amd.engine import label_counts
     cfg = pretrain_config(os.path.join(HERE, "configs", "bert_base_6layer_6conect.json"))
-    B = args.batch
     tr = Trainer(cfg, dev, lr=1e-4, warmup_steps=max(1, (args.steps + args.warmup) // 10),
-                 total_steps=10 * (args.steps + args.warmup), seed=1234, init=True, dtype=args.dtype)
+                 total_steps=10 * (args.steps + args.warmup), seed=1234, init=True, dtype=dtype)
     if world > 1:
         ddp = GradAllReducer(tr.engine.fp)
         ddp.broadcast_params(tr.engine.fp)
         tr.ddp = ddp
-    batch = synthetic_batch(cfg, B, dev, seed=1234 + rank)
-    T, P = batch["input_ids"].shape[1], batch["input_ids_pv"].shape[1]
+    batch = synthetic_batch(cfg, B, dev, seed=1234 + rank, T=shape["T"], P=shape["P"], n_boxes=shape["nbox"],
+                            n_triples=shape["n_triples"], npv=shape["npv"])
+    batch["_label_counts"] = label_counts(batch)   # known on the host when a loader builds the batch
+    T, P, R = shape["T"], shape["P"], shape["nbox"] + 1
     probe = GemmProbe(2 * B * T + 2 * B * P, cfg.intermediate_size, cfg.hidden_size)
     probe.install()
+    cprobe = CoattnProbe()
+    cprobe.install()
 
     def barrier():
         if world > 1:
-            import torch.distributed as dist
             dist.barrier()
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         tr.step(batch)
     barrier()
-    probe.active = True
+    probe.active = cprobe.active = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = tr.step(batch)
     barrier()
     dt = time.perf_counter() - t0
-    probe.active = False
+    probe.active = cprobe.active = False
+    per_rank = [dt]
     if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([dt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t)
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        gl = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(gl, t)
+        per_rank = [float(x) for x in gl]
+        dt = max(per_rank)
+    tr.watch.flush()
     loss = float(out["loss"])
     ms_step = 1000.0 * dt / args.steps
     value = world * B * args.steps / dt
@@ -191,43 +311,62 @@ def main():
     Mg, Ng, Kg = probe.key
     gemm_flops = 2.0 * Mg * Ng * Kg
     achieved = gemm_flops / (gemm_ms * 1e-3) if gemm_ms else None
-    bf = args.dtype == "bf16"
+    bf = dtype == "bf16"
     from k3m_amd import ops as _ops, _lib as _L
     x6 = not bf and _ops.F32_ALGO == _L.F32_SPLIT_BF16X6
     peak = PEAK_BF16_MFMA if bf else (PEAK_F32_X6 if x6 else PEAK_F32_MFMA)
     kname = "gemm_bf16_kernel" if bf else ("gemm_x6_kernel" if x6 else "gemm_f32_kernel")
+    traffic, traffic_src = pmc_traffic(probe.key, kname)
+    ref_sample = 3.0 * ref_fwd_flops(T, P, R, shape["n_triples"])
+    co_flops = 3.0 * coattn_fwd_flops(T, P, R) * B
+    co_ms = cprobe.total_ms() / args.steps if cprobe.events else None
     res = {
-        "metric": "pretrain samples/sec (whole job; bert_base_6layer_6conect, bs=64/GPU)",
+        "metric": "pretrain samples/sec (whole job; bert_base_6layer_6conect, bs=%d/GPU)" % B,
         "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": args.dtype, "data": "synthetic (SURVEY §8(d): random token ids, 36x2048 region feats, 10 PV triples)",
-        "config": {"workload": "config %d: bert_base_6layer_6conect %s bs=%d/GPU T=36 P=128 R=37 10 triples" % (
-                       3 if bf else 2, "bf16 encoder (fp32 master weights, heads, AdamW)" if bf else "fp32", B),
+        "dtype": dtype, "data": "synthetic (SURVEY §8(d): random token ids, %dx2048 region feats, %d PV triples)" % (
+            shape["nbox"], shape["n_triples"]),
+        "config": {"workload": "config %d: bert_base_6layer_6conect %s bs=%d/GPU T=%d P=%d R=%d %d triples" % (
+                       args.config, "bf16 encoder (fp32 master weights, heads, AdamW)" if bf else "fp32", B, T, P, R,
+                       shape["n_triples"]),
                    "model": "bert_base_6layer_6conect", "global_batch": B * world, "seq_len": T,
                    "parallelism": "dp%d" % world},
         "per_gpu_samples_s": round(value / world, 3),
         "loss": round(loss, 4),
-        "step_mfma_frac_vs_ref_flops": round(B * REF_FLOPS_PER_SAMPLE / (ms_step * 1e-3) / peak, 4),
+        "step_mfma_frac_vs_ref_flops": round(B * ref_sample / (ms_step * 1e-3) / peak, 4),
         "roofline": {"bound": "mfma", "kernel": "%s text-layer FFN1 %dx%dx%d" % (kname, Mg, Ng, Kg),
                      "achieved": round(achieved / 1e12, 2) if achieved else None,
                      "peak": peak / 1e12, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4) if achieved else None,
+                     "traffic": traffic,
                      "avg_launch_ms": round(gemm_ms, 4) if gemm_ms else None,
                      "launches": len(probe.events),
-                     "peak_basis": ("bf16 dense MFMA" if bf else "fp32 via 6 bf16 MFMA partial products = bf16 dense peak / 6"
-                                    if x6 else "f32 MFMA"),
-                     "traffic": pmc_traffic(probe.key, kname),
-                     "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/r1_gemm_ffn1_pmc.json)"},
+                     "algorithmic_flops_per_launch": gemm_flops,
+                     "peak_basis": ("bf16 dense MFMA" if bf else "fp32 via 6 bf16 MFMA partial products = bf16 dense "
+                                    "peak / 6" if x6 else "f32 MFMA"),
+                     "traffic_unit": "HBM bytes/launch (rocprofv3 PMC, %s)" % traffic_src if traffic else None},
+        "coattn": {"ms_per_step": round(co_ms, 3) if co_ms else None,
+                   "algorithmic_tflop_per_step": round(co_flops / 1e12, 3),
+                   "achieved": round(co_flops / (co_ms * 1e-3) / 1e12, 2) if co_ms else None,
+                   "frac": round(co_flops / (co_ms * 1e-3) / peak, 4) if co_ms else None,
+                   "scope": "18 co-attention layers fwd+bwd (lock-step blocks incl. attention and LayerNorm)"},
     }
+    if world > 1:
+        res["per_rank_s"] = [round(x, 4) for x in per_rank]
+        res["backend"] = args.backend
+        res["world_size_seen"] = dist.get_world_size()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_batch, args.cpu_steps)
+            res["cpu_baseline"] = cpu_baseline(cfg, shape, args.cpu_batch, args.cpu_steps)
         except Exception as e:  # baseline only; never masks the GPU result
             res["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(res), flush=True)
+    elif world > 1:
+        print("rank %d/%d: %.3f samples/s/GPU (%.1f ms/step)" % (rank, world, B * args.steps / per_rank[rank],
+                                                                1000.0 * per_rank[rank] / args.steps),
+              file=sys.stderr, flush=True)
     if world > 1:
-        import torch.distributed as dist
         dist.destroy_process_group()
 
 

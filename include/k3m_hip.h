@@ -208,16 +208,20 @@ int k3m_sa_attn_fwd(const float* T, const int32_t* nvalid, const int32_t* src, c
 int k3m_sa_attn_bwd(const float* dagg, const float* T, const float* att, const int32_t* nvalid,
                     const int32_t* src, const float* w2, float* dT, float* dw2, float* db2, float* dc_init, int batch,
                     int npv, int hidden, hipStream_t stream);
-/* LPM margin-ranking loss; ent_neg / val_neg [B, NPV, 2] int64 (-1 = none).  loss[0] = mean hinge.
- * Backward ACCUMULATES into dc_final [B,H] and the p/v thirds of dX. */
+/* LPM margin-ranking loss (:2469-2502); ent_neg [B, NPV, n_ent] / val_neg [B, NPV, n_val] int64 entity /
+ * value negative indices (-1 = none; n_ent = num_negative_pv // 2, n_val = num_negative_pv - n_ent,
+ * n_ent + n_val <= 16).  loss[0] = mean hinge over every (positive, negative) pair.
+ * ws: >= B*NPV*(2*(n_ent + n_val) + 1) + 2 floats.  Backward ACCUMULATES into dc_final [B,H] and the
+ * p/v thirds of dX. */
 int k3m_lpm_fwd(const float* c_final, const float* X, const int32_t* nvalid, const int64_t* ent_neg,
-                const int64_t* val_neg, int batch, int npv, int hidden, float margin, float* loss, float* ws,
-                hipStream_t stream);
+                const int64_t* val_neg, int batch, int npv, int hidden, int n_ent, int n_val, float margin,
+                float* loss, float* ws, hipStream_t stream);
 int k3m_lpm_bwd(const float* c_final, const float* X, const int32_t* nvalid, const int64_t* ent_neg,
-                const int64_t* val_neg, int batch, int npv, int hidden, float margin, const float* ws,
-                float* dc_final, float* dX, hipStream_t stream);
+                const int64_t* val_neg, int batch, int npv, int hidden, int n_ent, int n_val, float margin,
+                const float* ws, float* dc_final, float* dX, hipStream_t stream);
 /* Device-side draw of the LPM negatives with the reference's semantics (random.sample without
- * replacement of min(#candidates, 2) entity indices k != i and value indices j' != j). */
+ * replacement of min(#candidates, n_ent) entity indices k != i and min(#candidates, n_val) value
+ * indices j' != j, vilbert_k3m.py:2476-2492); unused slots are -1. */
 int k3m_lpm_sample(const int32_t* nvalid, int batch, int npv, int n_ent, int n_val, uint64_t seed, uint64_t off,
                    int64_t* ent_neg, int64_t* val_neg, hipStream_t stream);
 /* scatter the p / v gradients of dX back to the sequence rows and dX's c_init third into dc_init. */
@@ -233,6 +237,19 @@ int k3m_sa_gather_bwd(const float* dX, const int64_t* index_p, const int64_t* in
  * (1-beta, the bias-corrected step size, lr*wd) is formed in double and rounded once to fp32. */
 int k3m_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, long long n, double lr, double beta1,
               double beta2, double eps, double wd, int step, float grad_scale, hipStream_t stream);
+
+/* k3m_adamw with options (flags, OR-ed):
+ *   K3M_ADAM_ZERO_GRAD — g is zeroed after it is read (optimizer.step(); optimizer.zero_grad(),
+ *                        train_concap_struc.py:573-574, in one sweep of the gradient buffer);
+ *   K3M_ADAM_APEX      — apex FusedAdam(adam_w_mode) instead, the optimizer of the mixed-precision
+ *                        branches (:410-411, :426): p -= lr*((m/bc1)/(sqrt(v/bc2)+eps) + wd*p), with
+ *                        bc = 1 unless K3M_ADAM_APEX_BIAS_CORRECTION (the driver passes
+ *                        bias_correction=False). */
+#define K3M_ADAM_ZERO_GRAD 1
+#define K3M_ADAM_APEX 2
+#define K3M_ADAM_APEX_BIAS_CORRECTION 4
+int k3m_adamw_ex(float* p, float* g, float* m, float* v, uint16_t* p_bf16, long long n, double lr, double beta1,
+                 double beta2, double eps, double wd, int step, float grad_scale, int flags, hipStream_t stream);
 
 /* Attention for sequences longer than 128 (up to 512 keys, d <= 128): the fine-tuning PV text
  * (max_seq_length_pv 256, finetune.py:1275) and SURVEY config 5 (P = 320).  Same arguments,

@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(_HERE, "libk3m_hip.so")
 F32, BF16 = 0, 1
 EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_DGELU, EPI_BIAS_SIGMOID = 0, 1, 2, 3, 4
 F32_SPLIT_BF16X6, F32_MFMA_F32 = 0, 1
+ADAM_ZERO_GRAD, ADAM_APEX, ADAM_APEX_BIAS_CORRECTION = 1, 2, 4
 
 vp, i32, i64, f32, u64 = C.c_void_p, C.c_int, C.c_longlong, C.c_float, C.c_uint64
 
@@ -61,11 +62,13 @@ SIGNATURES = {
     "k3m_sa_gather": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
     "k3m_sa_attn_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp],
     "k3m_sa_attn_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp],
-    "k3m_lpm_fwd": [vp, vp, vp, vp, vp, i32, i32, i32, f32, vp, vp, vp],
-    "k3m_lpm_bwd": [vp, vp, vp, vp, vp, i32, i32, i32, f32, vp, vp, vp, vp],
+    "k3m_lpm_fwd": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, f32, vp, vp, vp],
+    "k3m_lpm_bwd": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, f32, vp, vp, vp, vp],
     "k3m_lpm_sample": [vp, i32, i32, i32, i32, u64, u64, vp, vp, vp],
     "k3m_sa_gather_bwd": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
     "k3m_adamw": [vp, vp, vp, vp, vp, i64, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double, i32, f32, vp],
+    "k3m_adamw_ex": [vp, vp, vp, vp, vp, i64, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double, i32, f32,
+                     i32, vp],
     "k3m_cast_f32_bf16": [vp, vp, i64, vp],
     "k3m_convert": [vp, i32, vp, i32, i64, i32, f32, vp],
     "k3m_add_inplace": [vp, vp, i64, f32, i32, vp],

@@ -75,7 +75,90 @@ __global__ __launch_bounds__(256) void adamw_torch_kernel(float* __restrict__ p,
   }
 }
 
+// k3m_adamw_ex: the pytorch_transformers rule above or apex FusedAdam (adam_w_mode, the mixed-
+// precision branch train_concap_struc.py:410-411, :426): m, v as above;
+//   p -= lr * ((m / bc1) / (sqrt(v / bc2) + eps) + wd * p)      (bc = 1 without bias correction)
+// flags & K3M_ADAM_ZERO_GRAD: g is zeroed after it is read (optimizer.zero_grad() fused: the
+// gradient buffer is not swept a second time).
+template <bool APEX, bool ZERO>
+__global__ __launch_bounds__(256) void adamw_ex_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                       float* __restrict__ m, float* __restrict__ v,
+                                                       uint16_t* __restrict__ pb, long long n4, float b1, float omb1,
+                                                       float b2, float omb2, float eps, float step_size, float decay,
+                                                       float gscale, float rbc1, float rbc2) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    floatx4 pp = reinterpret_cast<floatx4*>(p)[i];
+    floatx4 gg = reinterpret_cast<const floatx4*>(g)[i];
+    floatx4 mm = reinterpret_cast<floatx4*>(m)[i];
+    floatx4 vv = reinterpret_cast<floatx4*>(v)[i];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float gr = gg[q] * gscale;
+      mm[q] = __fadd_rn(__fmul_rn(mm[q], b1), __fmul_rn(omb1, gr));
+      vv[q] = __fadd_rn(__fmul_rn(vv[q], b2), __fmul_rn(__fmul_rn(omb2, gr), gr));
+      if constexpr (APEX) {
+        const float denom = __fadd_rn(sqrtf(__fmul_rn(vv[q], rbc2)), eps);
+        const float upd = __fadd_rn(__fdiv_rn(__fmul_rn(mm[q], rbc1), denom), __fmul_rn(decay, pp[q]));
+        pp[q] = __fsub_rn(pp[q], __fmul_rn(step_size, upd));
+      } else {
+        const float denom = sqrtf(vv[q]) + eps;
+        pp[q] = __fadd_rn(pp[q], __fmul_rn(-step_size, __fdiv_rn(mm[q], denom)));
+        if (decay != 0.f) pp[q] = __fadd_rn(pp[q], __fmul_rn(-decay, pp[q]));
+      }
+    }
+    reinterpret_cast<floatx4*>(p)[i] = pp;
+    reinterpret_cast<floatx4*>(m)[i] = mm;
+    reinterpret_cast<floatx4*>(v)[i] = vv;
+    if constexpr (ZERO) reinterpret_cast<floatx4*>(g)[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (pb) {
+      uint2 u;
+      u.x = (uint32_t)from_f<bf16_t>(pp[0]).x | ((uint32_t)from_f<bf16_t>(pp[1]).x << 16);
+      u.y = (uint32_t)from_f<bf16_t>(pp[2]).x | ((uint32_t)from_f<bf16_t>(pp[3]).x << 16);
+      reinterpret_cast<uint2*>(pb)[i] = u;
+    }
+  }
+}
+
 }  // namespace
+
+extern "C" int k3m_adamw_ex(float* p, float* g, float* m, float* v, uint16_t* p_bf16, long long n, double lr,
+                            double beta1, double beta2, double eps, double wd, int step, float grad_scale, int flags,
+                            hipStream_t st) {
+  K3M_ARG(p && g && m && v && n >= 0 && n % 4 == 0 && step >= 1);
+  K3M_ARG(((uintptr_t)p & 15) == 0 && ((uintptr_t)g & 15) == 0 && ((uintptr_t)m & 15) == 0 && ((uintptr_t)v & 15) == 0);
+  K3M_ARG((flags & ~(K3M_ADAM_ZERO_GRAD | K3M_ADAM_APEX | K3M_ADAM_APEX_BIAS_CORRECTION)) == 0);
+  if (n == 0) return 0;
+  const long long n4 = n / 4;
+  const int blocks = (int)std::min<long long>((n4 + 255) / 256, 256 * 16);
+  const bool apex = (flags & K3M_ADAM_APEX) != 0, zero = (flags & K3M_ADAM_ZERO_GRAD) != 0;
+  float step_size, decay, rbc1 = 1.f, rbc2 = 1.f;
+  if (apex) {
+    if (flags & K3M_ADAM_APEX_BIAS_CORRECTION) {
+      rbc1 = (float)(1.0 / (1.0 - std::pow(beta1, step)));
+      rbc2 = (float)(1.0 / (1.0 - std::pow(beta2, step)));
+    }
+    step_size = (float)lr;
+    decay = (float)wd;
+  } else {
+    const double bc1 = 1.0 - std::pow(beta1, step), bc2 = 1.0 - std::pow(beta2, step);
+    step_size = (float)(lr * std::sqrt(bc2) / bc1);
+    decay = wd > 0.0 ? (float)(lr * wd) : 0.f;
+  }
+#define K3M_ADAM_LAUNCH(A, Z)                                                                                      \
+  hipLaunchKernelGGL((adamw_ex_kernel<A, Z>), dim3(blocks), dim3(256), 0, st, p, g, m, v, p_bf16, n4, (float)beta1, \
+                     (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps, step_size, decay,         \
+                     grad_scale, rbc1, rbc2)
+  if (apex) {
+    if (zero) K3M_ADAM_LAUNCH(true, true);
+    else K3M_ADAM_LAUNCH(true, false);
+  } else {
+    if (zero) K3M_ADAM_LAUNCH(false, true);
+    else K3M_ADAM_LAUNCH(false, false);
+  }
+#undef K3M_ADAM_LAUNCH
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int k3m_adamw_torch(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, long long n, double lr,
                                double beta1, double beta2, double eps, double wd, int step, float grad_scale,

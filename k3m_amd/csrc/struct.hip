@@ -26,18 +26,32 @@ __device__ __forceinline__ int count_valid(const int64_t* index_p, int i, int np
   return n;
 }
 
-__global__ void sa_count_kernel(const int64_t* index_p, int batch, int npv, int32_t* nvalid, int32_t* src) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  int last = -1;
-  for (int i = 0; i < batch; ++i) {
-    const int n = count_valid(index_p, i, npv);
-    nvalid[i] = n;
-    if (n > 0) {
-      src[i] = i;
-      last = i;
-    } else {
-      src[i] = last;  // -1 -> c_initial[0]
+// nvalid[i] and src[i] (the latest item k <= i with triples, -1 if none) for every item: one
+// 1024-thread workgroup, one item per thread, an inclusive max-scan per 1024-item chunk carried
+// across chunks (was a single serial thread: 101 us per step at B = 64).
+constexpr int CNT_NT = 1024;
+__global__ __launch_bounds__(CNT_NT) void sa_count_kernel(const int64_t* index_p, int batch, int npv, int32_t* nvalid,
+                                                          int32_t* src) {
+  __shared__ int scan[CNT_NT];
+  int carry = -1;
+  for (int base = 0; base < batch; base += CNT_NT) {
+    const int i = base + (int)threadIdx.x;
+    int n = 0;
+    if (i < batch) {
+      n = count_valid(index_p, i, npv);
+      nvalid[i] = n;
     }
+    scan[threadIdx.x] = (i < batch && n > 0) ? i : -1;
+    __syncthreads();
+    for (int d = 1; d < CNT_NT; d <<= 1) {
+      const int o = threadIdx.x >= (unsigned)d ? scan[threadIdx.x - d] : -1;
+      __syncthreads();
+      scan[threadIdx.x] = max(scan[threadIdx.x], o);
+      __syncthreads();
+    }
+    if (i < batch) src[i] = max(carry, scan[threadIdx.x]);   // -1 -> c_initial[0]
+    carry = max(carry, scan[CNT_NT - 1]);
+    __syncthreads();
   }
 }
 
@@ -144,25 +158,29 @@ __global__ __launch_bounds__(NT) void sa_attn_bwd_kernel(const float* dagg, cons
   if (threadIdx.x == 0) atomicAdd(db2, db);
 }
 
-// pair p of triple (i, j): e = 0,1 entity negatives; e = 2,3 value negatives
-__device__ __forceinline__ bool pair_neg(const int64_t* ent, const int64_t* val, long long ij, int e, int& k) {
-  const long long v = e < 2 ? ent[ij * 2 + e] : val[ij * 2 + (e - 2)];
+// negative e of triple ij: e < ke entity negatives (ent[ij*ke + e]), then kv value negatives
+constexpr int LPM_KMAX = 16;
+__device__ __forceinline__ bool pair_neg(const int64_t* ent, const int64_t* val, long long ij, int e, int ke, int kv,
+                                         int& k) {
+  const long long v = e < ke ? ent[ij * ke + e] : val[ij * kv + (e - ke)];
   k = (int)v;
   return v >= 0;
 }
 
-// ws layout: [B*npv*4] hinge (-1 = no pair), [B*npv] pos norm, [B*npv*4] neg norm, [2] (count, sum)
+// ws layout (K = ke + kv): [B*npv*K] hinge (-1 = no pair), [B*npv] pos norm, [B*npv*K] neg norm,
+// [2] (count, sum)
 __global__ __launch_bounds__(NT) void lpm_fwd_kernel(const float* cf, const float* X, const int32_t* nvalid,
-                                                     const int64_t* ent, const int64_t* val, int npv, int h,
-                                                     float margin, float* ws, int total) {
+                                                     const int64_t* ent, const int64_t* val, int npv, int h, int ke,
+                                                     int kv, float margin, float* ws, int total) {
   __shared__ float red[4];
+  const int K = ke + kv;
   const int i = blockIdx.x / npv, j = blockIdx.x % npv;
   const long long ij = blockIdx.x;
   float* hinge = ws;
-  float* posn = ws + (long long)total * 4;
+  float* posn = ws + (long long)total * K;
   float* negn = posn + total;
   if (j >= nvalid[i]) {
-    if (threadIdx.x < 4) hinge[ij * 4 + threadIdx.x] = -1.f;
+    if ((int)threadIdx.x < K) hinge[ij * K + threadIdx.x] = -1.f;
     return;
   }
   const float* x = X + ij * 3 * h;
@@ -173,32 +191,32 @@ __global__ __launch_bounds__(NT) void lpm_fwd_kernel(const float* cf, const floa
   }
   const float pn = sqrtf(block_sum<4>(a, red));
   if (threadIdx.x == 0) posn[ij] = pn;
-  for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < K; ++e) {
     int k;
-    const bool has = pair_neg(ent, val, ij, e, k);
+    const bool has = pair_neg(ent, val, ij, e, ke, kv, k);
     if (!has) {
-      if (threadIdx.x == 0) hinge[ij * 4 + e] = -1.f;
+      if (threadIdx.x == 0) hinge[ij * K + e] = -1.f;
       continue;
     }
     float b = 0.f;
     for (int c = threadIdx.x; c < h; c += NT) {
       float u;
-      if (e < 2) u = cf[(long long)k * h + c] + x[h + c] - x[2 * h + c];
+      if (e < ke) u = cf[(long long)k * h + c] + x[h + c] - x[2 * h + c];
       else u = cf[(long long)i * h + c] + x[h + c] - X[((long long)i * npv + k) * 3 * h + 2 * h + c];
       b += u * u;
     }
     const float nn = sqrtf(block_sum<4>(b, red));
     if (threadIdx.x == 0) {
-      negn[ij * 4 + e] = nn;
-      hinge[ij * 4 + e] = fmaxf(0.f, nn - pn + margin);
+      negn[ij * K + e] = nn;
+      hinge[ij * K + e] = fmaxf(0.f, nn - pn + margin);
     }
   }
 }
 
-__global__ __launch_bounds__(NT) void lpm_reduce_kernel(float* ws, int total, float* loss) {
+__global__ __launch_bounds__(NT) void lpm_reduce_kernel(float* ws, int total, int K, float* loss) {
   __shared__ float red[4];
   float cnt = 0.f, sum = 0.f;
-  for (int p = threadIdx.x; p < total * 4; p += NT) {
+  for (int p = threadIdx.x; p < total * K; p += NT) {
     const float hv = ws[p];
     if (hv >= 0.f) {
       cnt += 1.f;
@@ -208,7 +226,7 @@ __global__ __launch_bounds__(NT) void lpm_reduce_kernel(float* ws, int total, fl
   cnt = block_sum<4>(cnt, red);
   sum = block_sum<4>(sum, red);
   if (threadIdx.x == 0) {
-    float* tail = ws + (long long)total * 9;
+    float* tail = ws + (long long)total * (2 * K + 1);
     tail[0] = cnt;
     tail[1] = sum;
     loss[0] = cnt > 0.f ? sum / cnt : NAN;  // mean of an empty tensor is NaN, as in the reference
@@ -216,29 +234,31 @@ __global__ __launch_bounds__(NT) void lpm_reduce_kernel(float* ws, int total, fl
 }
 
 __global__ __launch_bounds__(NT) void lpm_bwd_kernel(const float* cf, const float* X, const int32_t* nvalid,
-                                                     const int64_t* ent, const int64_t* val, int npv, int h,
-                                                     const float* ws, int total, float* dcf, float* dX) {
+                                                     const int64_t* ent, const int64_t* val, int npv, int h, int ke,
+                                                     int kv, const float* ws, int total, float* dcf, float* dX) {
+  const int K = ke + kv;
   const int i = blockIdx.x / npv, j = blockIdx.x % npv;
   const long long ij = blockIdx.x;
   if (j >= nvalid[i]) return;
   const float* hinge = ws;
-  const float* posn = ws + (long long)total * 4;
+  const float* posn = ws + (long long)total * K;
   const float* negn = posn + total;
-  const float cnt = ws[(long long)total * 9];
+  const float cnt = ws[(long long)total * (2 * K + 1)];
   const float w = 1.f / cnt;
   const float* x = X + ij * 3 * h;
   float* dx = dX + ij * 3 * h;
   // coefficient of the positive norm: -w per active pair
   float cpos = 0.f;
-  float cneg[4];
-  int kk[4];
-  for (int e = 0; e < 4; ++e) {
+  float cneg[LPM_KMAX];
+  int kk[LPM_KMAX];
+#pragma unroll
+  for (int e = 0; e < LPM_KMAX; ++e) {
     cneg[e] = 0.f;
     kk[e] = -1;
     int k;
-    if (pair_neg(ent, val, ij, e, k) && hinge[ij * 4 + e] > 0.f) {
+    if (e < K && pair_neg(ent, val, ij, e, ke, kv, k) && hinge[ij * K + e] > 0.f) {
       cpos -= w;
-      cneg[e] = w / fmaxf(negn[ij * 4 + e], 1e-30f);
+      cneg[e] = w / fmaxf(negn[ij * K + e], 1e-30f);
       kk[e] = k;
     }
   }
@@ -247,9 +267,10 @@ __global__ __launch_bounds__(NT) void lpm_bwd_kernel(const float* cf, const floa
     const float p = x[h + c], v = x[2 * h + c];
     const float up = cf[(long long)i * h + c] + p - v;
     float gci = cp * up, gp = cp * up, gv = -cp * up;
-    for (int e = 0; e < 4; ++e) {
+#pragma unroll
+    for (int e = 0; e < LPM_KMAX; ++e) {
       if (kk[e] < 0) continue;
-      if (e < 2) {
+      if (e < ke) {
         const float u = cf[(long long)kk[e] * h + c] + p - v;
         const float g = cneg[e] * u;
         atomicAdd(dcf + (long long)kk[e] * h + c, g);
@@ -270,41 +291,38 @@ __global__ __launch_bounds__(NT) void lpm_bwd_kernel(const float* cf, const floa
   }
 }
 
-// reference draw: random.sample(candidates, min(len, n)) without replacement
+// random.sample(range(nc), take) semantics: `take` distinct ranks drawn uniformly without replacement
+// (draw q picks uniformly among the nc - q ranks not drawn yet: the r-th free rank, found by stepping
+// over the earlier draws in ascending order), then rank -> index skipping `self`.
+__device__ __forceinline__ void sample_distinct(uint64_t seed, uint64_t base, int nc, int take, int self,
+                                                int64_t* out) {
+  int drawn[LPM_KMAX];   // ascending
+  for (int q = 0; q < take; ++q) {
+    int r = (int)(k3m_hash(seed, base + q) % (uint32_t)(nc - q));
+    int pos = 0;
+    for (; pos < q; ++pos) {
+      if (r >= drawn[pos]) ++r;
+      else break;
+    }
+    for (int s = q; s > pos; --s) drawn[s] = drawn[s - 1];
+    drawn[pos] = r;
+    out[q] = r >= self ? r + 1 : r;
+  }
+}
+
 __global__ void lpm_sample_kernel(const int32_t* nvalid, int batch, int npv, int n_ent, int n_val, uint64_t seed,
                                   uint64_t off, int64_t* ent, int64_t* val) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= batch * npv) return;
   const int i = t / npv, j = t % npv;
-  ent[t * 2] = ent[t * 2 + 1] = -1;
-  val[t * 2] = val[t * 2 + 1] = -1;
+  for (int q = 0; q < n_ent; ++q) ent[(long long)t * n_ent + q] = -1;
+  for (int q = 0; q < n_val; ++q) val[(long long)t * n_val + q] = -1;
   const int n = nvalid[i];
   if (j >= n) return;
-  const uint64_t base = off + (uint64_t)t * 4;
-  // entity candidates: all k != i
-  {
-    const int nc = batch - 1, take = min(nc, min(n_ent, 2));
-    int first = -1;
-    for (int q = 0; q < take; ++q) {
-      const int m = nc - q;
-      int r = (int)(k3m_hash(seed, base + q) % (uint32_t)m);
-      if (q == 1 && r >= first) r += 1;  // skip the already drawn candidate rank
-      if (q == 0) first = r;
-      const int k = r >= i ? r + 1 : r;  // rank among candidates -> item index
-      ent[t * 2 + q] = k;
-    }
-  }
-  {
-    const int nc = n - 1, take = min(nc, min(n_val, 2));
-    int first = -1;
-    for (int q = 0; q < take; ++q) {
-      const int m = nc - q;
-      int r = (int)(k3m_hash(seed, base + 2 + q) % (uint32_t)m);
-      if (q == 1 && r >= first) r += 1;
-      if (q == 0) first = r;
-      val[t * 2 + q] = r >= j ? r + 1 : r;
-    }
-  }
+  const uint64_t base = off + (uint64_t)t * (n_ent + n_val);
+  // entity candidates: all k != i (vilbert_k3m.py:2476-2480); value candidates: j' != j (:2488-2492)
+  sample_distinct(seed, base, batch - 1, min(batch - 1, n_ent), i, ent + (long long)t * n_ent);
+  sample_distinct(seed, base + n_ent, n - 1, min(n - 1, n_val), j, val + (long long)t * n_val);
 }
 
 template <typename T>
@@ -335,7 +353,7 @@ extern "C" int k3m_sa_gather(const void* seq, const int64_t* index_p, const int6
   K3M_ARG(seq && index_p && index_v && c_init && X && nvalid && src && npv > 0 && npv <= 64);
   K3M_ARG(dtype == K3M_F32);
   if (batch == 0) return 0;
-  hipLaunchKernelGGL(sa_count_kernel, dim3(1), dim3(64), 0, st, index_p, batch, npv, nvalid, src);
+  hipLaunchKernelGGL(sa_count_kernel, dim3(1), dim3(CNT_NT), 0, st, index_p, batch, npv, nvalid, src);
   hipLaunchKernelGGL(sa_gather_kernel<float>, dim3(batch * npv), dim3(NT), 0, st, (const float*)seq, index_p, index_v,
                      c_init, X, nvalid, len, npv, hidden);
   K3M_CHECK_LAUNCH();
@@ -365,34 +383,37 @@ extern "C" int k3m_sa_attn_bwd(const float* dagg, const float* T, const float* a
 }
 
 extern "C" int k3m_lpm_fwd(const float* c_final, const float* X, const int32_t* nvalid, const int64_t* ent_neg,
-                           const int64_t* val_neg, int batch, int npv, int hidden, float margin, float* loss, float* ws,
-                           hipStream_t st) {
-  K3M_ARG(c_final && X && nvalid && ent_neg && val_neg && loss && ws);
+                           const int64_t* val_neg, int batch, int npv, int hidden, int n_ent, int n_val, float margin,
+                           float* loss, float* ws, hipStream_t st) {
+  K3M_ARG(c_final && X && nvalid && loss && ws && n_ent >= 0 && n_val >= 0 && n_ent + n_val <= LPM_KMAX);
+  K3M_ARG((ent_neg || n_ent == 0) && (val_neg || n_val == 0));
   const int total = batch * npv;
   if (total == 0) return 0;
   hipLaunchKernelGGL(lpm_fwd_kernel, dim3(total), dim3(NT), 0, st, c_final, X, nvalid, ent_neg, val_neg, npv, hidden,
-                     margin, ws, total);
-  hipLaunchKernelGGL(lpm_reduce_kernel, dim3(1), dim3(NT), 0, st, ws, total, loss);
+                     n_ent, n_val, margin, ws, total);
+  hipLaunchKernelGGL(lpm_reduce_kernel, dim3(1), dim3(NT), 0, st, ws, total, n_ent + n_val, loss);
   K3M_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int k3m_lpm_bwd(const float* c_final, const float* X, const int32_t* nvalid, const int64_t* ent_neg,
-                           const int64_t* val_neg, int batch, int npv, int hidden, float margin, const float* ws,
-                           float* dc_final, float* dX, hipStream_t st) {
-  K3M_ARG(c_final && X && nvalid && ent_neg && val_neg && ws && dc_final && dX);
+                           const int64_t* val_neg, int batch, int npv, int hidden, int n_ent, int n_val, float margin,
+                           const float* ws, float* dc_final, float* dX, hipStream_t st) {
+  K3M_ARG(c_final && X && nvalid && ws && dc_final && dX && n_ent >= 0 && n_val >= 0 && n_ent + n_val <= LPM_KMAX);
+  K3M_ARG((ent_neg || n_ent == 0) && (val_neg || n_val == 0));
   (void)margin;
   const int total = batch * npv;
   if (total == 0) return 0;
   hipLaunchKernelGGL(lpm_bwd_kernel, dim3(total), dim3(NT), 0, st, c_final, X, nvalid, ent_neg, val_neg, npv, hidden,
-                     ws, total, dc_final, dX);
+                     n_ent, n_val, ws, total, dc_final, dX);
   K3M_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int k3m_lpm_sample(const int32_t* nvalid, int batch, int npv, int n_ent, int n_val, uint64_t seed,
                               uint64_t off, int64_t* ent_neg, int64_t* val_neg, hipStream_t st) {
-  K3M_ARG(nvalid && ent_neg && val_neg);
+  K3M_ARG(nvalid && n_ent >= 0 && n_val >= 0 && n_ent + n_val <= LPM_KMAX);
+  K3M_ARG((ent_neg || n_ent == 0) && (val_neg || n_val == 0));
   const int total = batch * npv;
   if (total == 0) return 0;
   hipLaunchKernelGGL(lpm_sample_kernel, dim3(k3m_cdiv(total, 256)), dim3(256), 0, st, nvalid, batch, npv, n_ent, n_val,

@@ -225,9 +225,16 @@ class RegionCollator(object):
         if self.F % 4:
             raise ValueError("v_feature_size must be a multiple of 4")
         self._stage = None
+        self._copied = None
 
     def _staging(self, B):
         t = self.torch
+        if self._copied is not None:
+            # the previous batch's host->device copies read this staging buffer: they must have
+            # landed before it is overwritten (a loader running ahead of the GPU would otherwise
+            # hand the previous batch the next batch's features)
+            self._copied.synchronize()
+            self._copied = None
         if self._stage is None or self._stage[0].shape[0] < B:
             pin = self.device.type == "cuda"
             ct = self.F if self.visual_target else self.Ct
@@ -255,6 +262,9 @@ class RegionCollator(object):
             tgt = feat_d.clone()        # image_target = unmasked features (dataset:594-596)
         else:
             tgt = tgt_h.to(dev, non_blocking=nbk)
+        if nbk:
+            self._copied = t.cuda.Event()
+            self._copied.record()
         zero = t.from_numpy(np.stack([s.zero_feat for s in samples])).to(dev, non_blocking=nbk)
         mlab = t.from_numpy(np.stack([s.masked_label for s in samples])).to(dev, non_blocking=nbk)
         image_feat = t.empty((B, R + 1, F), dtype=t.float32, device=dev)
@@ -281,6 +291,10 @@ class RegionCollator(object):
                      image_label=d(np.stack([s.image_label for s in samples])), image_mask=d(imask),
                      index_p=d(np.stack([s.index_p for s in samples])),
                      index_v=d(np.stack([s.index_v for s in samples])))
+        # labelled-row counts of the heads, known here on the host (engine.label_counts): the
+        # forward then sizes its compacted head buffers without a device->host sync
+        batch["_label_counts"] = (int((text[:, 3] >= 0).sum()) + int((pv[:, 3] >= 0).sum()),
+                                  int(sum(int((s.image_label >= 1).sum()) for s in samples)))
         return batch, [s.item_id for s in samples]
 
 

@@ -462,6 +462,15 @@ def _lockstep(gens):
         live = nxt
 
 
+def label_counts(batch):
+    """(masked-LM labels of text + PV, masked regions): the row counts of the labelled-row heads.
+    A loader that builds the batch on the host stores them as batch["_label_counts"] so the forward
+    needs no device->host sync; this helper computes them from a batch (one sync)."""
+    n_m = int((batch["lm_label_ids"] >= 0).sum()) + int((batch["lm_label_ids_pv"] >= 0).sum())
+    n_v = int((batch["image_label"] >= 1).sum())
+    return (n_m, n_v)
+
+
 def _ext_mask(m):
     # (1 - mask) * -10000 additive key mask (vilbert_k3m.py:2547-2580); input marshalling
     return ((1.0 - m.to(torch.float32)) * -10000.0).contiguous()
@@ -778,20 +787,22 @@ class K3MEngine(object):
             return {"c_initial": c_init, "c_final": c_final, "pooled_t": pooled_t, "pooled_pv": pooled_pv,
                     "pooled_v": pooled_v}, ctx
         assert groups == 1
+        nneg = int(getattr(c, "num_negative_pv", 4))
         if ent_neg is None:
-            ent_neg = torch.empty((B, NPV, 2), dtype=torch.int64, device=dev)
-            val_neg = torch.empty((B, NPV, 2), dtype=torch.int64, device=dev)
-            nneg = getattr(c, "num_negative_pv", 4)
-            L.call("k3m_lpm_sample", nvalid.data_ptr(), B, NPV, nneg // 2, nneg - nneg // 2, rng.seed,
-                   rng.take(B * NPV * 4), ent_neg.data_ptr(), val_neg.data_ptr(), L.stream())
+            ke, kv = nneg // 2, nneg - nneg // 2   # vilbert_k3m.py:2476, :2488
+            ent_neg = torch.empty((B, NPV, ke), dtype=torch.int64, device=dev)
+            val_neg = torch.empty((B, NPV, kv), dtype=torch.int64, device=dev)
+            L.call("k3m_lpm_sample", nvalid.data_ptr(), B, NPV, ke, kv, rng.seed, rng.take(B * NPV * (ke + kv)),
+                   L.ptr(ent_neg), L.ptr(val_neg), L.stream())
         else:
             ent_neg = ent_neg.to(device=dev, dtype=torch.int64).contiguous()
             val_neg = val_neg.to(device=dev, dtype=torch.int64).contiguous()
+            ke, kv = ent_neg.shape[2], val_neg.shape[2]
         lpm = torch.empty((1,), dtype=torch.float32, device=dev)
-        lws = torch.empty((B * NPV * 9 + 2,), dtype=torch.float32, device=dev)
+        lws = torch.empty((B * NPV * (2 * (ke + kv) + 1) + 2,), dtype=torch.float32, device=dev)
         margin = float(getattr(c, "margin", 1.0))
-        L.call("k3m_lpm_fwd", c_final.data_ptr(), X.data_ptr(), nvalid.data_ptr(), ent_neg.data_ptr(),
-               val_neg.data_ptr(), B, NPV, H, margin, lpm.data_ptr(), lws.data_ptr(), L.stream())
+        L.call("k3m_lpm_fwd", c_final.data_ptr(), X.data_ptr(), nvalid.data_ptr(), L.ptr(ent_neg), L.ptr(val_neg), B, NPV,
+               H, ke, kv, margin, lpm.data_ptr(), lws.data_ptr(), L.stream())
         ctx["struct"] = (X, nvalid, src, Tm, att, agg, c_init, c_final, ent_neg, val_neg, lws, index_p, index_v, NPV,
                          margin)
 
@@ -816,7 +827,11 @@ class K3MEngine(object):
         L.call("k3m_compact_labels_ex", batch["image_label"].contiguous().data_ptr(), B * R1, 1, R1, R, 1, 2,
                idx_v.data_ptr(), None, src_v.data_ptr(), sc_v.data_ptr(), sl_v.data_ptr(), cnt_v.data_ptr(),
                L.stream())
-        n_m, n_v = [int(x) for x in cnt.tolist()]   # one host sync per step (labelled-row counts)
+        hint = batch.get("_label_counts")
+        if hint is not None:   # counted on the host when the batch was built (label_counts): no sync
+            n_m, n_v = int(hint[0]), int(hint[1])
+        else:
+            n_m, n_v = [int(x) for x in cnt.tolist()]   # host sync (labelled-row counts)
 
         V = c.vocab_size
         hm = torch.empty((n_m, H), dtype=torch.float32, device=dev)
@@ -926,8 +941,9 @@ class K3MEngine(object):
         dcf = torch.zeros_like(c_final)
         dX = torch.zeros_like(X)
         if lws is not None:
-            L.call("k3m_lpm_bwd", c_final.data_ptr(), X.data_ptr(), nvalid.data_ptr(), ent_neg.data_ptr(),
-                   val_neg.data_ptr(), B, NPV, H, margin, lws.data_ptr(), dcf.data_ptr(), dX.data_ptr(), L.stream())
+            L.call("k3m_lpm_bwd", c_final.data_ptr(), X.data_ptr(), nvalid.data_ptr(), L.ptr(ent_neg), L.ptr(val_neg), B,
+                   NPV, H, ent_neg.shape[2], val_neg.shape[2], margin, lws.data_ptr(), dcf.data_ptr(), dX.data_ptr(),
+                   L.stream())
             if w_lpm != 1.0:
                 ops.add_(dcf, dcf.clone(), w_lpm - 1.0)
                 ops.add_(dX, dX.clone(), w_lpm - 1.0)

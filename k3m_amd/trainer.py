@@ -1,24 +1,76 @@
-"""The pretraining step: forward + backward + (DDP all-reduce) + AdamW + WarmupLinearSchedule.
+"""The pretraining step: forward + backward + (DDP all-reduce) + optimizer + LR schedule.
 
-Mirrors the driver loop of train_concap_struc.py:466-589 with the fp32 optimizer branch
-(:434-448): pytorch_transformers AdamW(lr, eps=1e-8, betas=(0.9, 0.98)), weight decay 0.01 on
-every parameter except names containing "bias"/"LayerNorm.bias"/"LayerNorm.weight" (:352-367),
-WarmupLinearSchedule stepped after the optimizer (:588) so step s runs at lr * lambda(s) and the
-first step at lr = 0.  loss = mlm_t + img * loss_img_weight + mlm_pv + lpm (:531-533).
+Mirrors the driver loop of train_concap_struc.py:466-589.
+
+* Optimizer (A14).  Default: the fp32 branch (:434-448), pytorch_transformers AdamW(lr, eps=1e-8,
+  betas=(0.9, 0.98)).  ``optimizer="fused_adam"``: the mixed-precision branches (:397-433), apex
+  FusedAdam(bias_correction=False, betas (0.9, 0.999)); the per-group weight decay (0.01 / 0.0) of
+  the parameter groups overrides FusedAdam's default 5e-4, as torch param groups do.
+* Parameter groups (:352-389).  Weight decay 0.01 on every name without "bias" / "LayerNorm.bias" /
+  "LayerNorm.weight".  With a pretrained model each tensor is its own group and the names of the
+  BERT weight-name file run at lr x 0.1 (``lr_mult``: name -> multiplier; ``bert_lr_mult`` builds
+  it with the driver's ``key[12:]`` rule).  ``frozen_names`` (``--freeze``, :243-260) are skipped.
+  Tensors of equal (weight decay, multiplier) that are adjacent in the flat buffer are ONE launch.
+* Schedule.  WarmupLinearSchedule stepped after the optimizer (:588), so step s runs at
+  lr * lambda(s) and the first step at lr = 0.  ``lr_schedule="warmup_linear_fp16"``: the --fp16
+  branch (:579-584), where only ``param_groups[0]`` is re-set to lr * warmup_linear(step / t_total,
+  warmup_proportion) and every other group keeps the 0 that WarmupLinearSchedule's constructor
+  assigned (reproduced as the reference runs; not the default).
+* Gradient accumulation (:561-575): each micro-step back-propagates loss / accum_steps; the
+  optimizer (and the DDP all-reduce) run on every accum_steps-th call.
+* ``objective == 1`` label rewrite (:481-494) before the forward.
+* loss = mlm_t + img * loss_img_weight + mlm_pv + lpm (:531-533), the optimised objective.
+* NaN fail-fast: every step's loss is copied to pinned host memory behind an event and
+  checked a step later, without a host synchronisation; a non-finite loss raises FloatingPointError.
 """
+import collections
 import math
 
 import torch
 
 from . import _lib as L
 from .engine import K3MEngine
-from .params import param_spec
+from .params import param_spec, segment_of
 
 
 def warmup_linear_lambda(step, warmup, t_total):
+    """pytorch_transformers 1.1.0 WarmupLinearSchedule.lr_lambda."""
     if step < warmup:
         return float(step) / float(max(1, warmup))
     return max(0.0, float(t_total - step) / float(max(1.0, t_total - warmup)))
+
+
+def warmup_linear_fp16(x, warmup=0.002):
+    """train_concap_struc.py:60-65 (the --fp16 branch's manual schedule, x = step / t_total)."""
+    if x < warmup:
+        return x / warmup
+    return max((x - 1.) / (warmup - 1.), 0)
+
+
+def bert_lr_mult(names, bert_weight_names, ddp=True, mult=0.1):
+    """lr multipliers of the pretrained-model parameter groups (train_concap_struc.py:369-375): a
+    parameter whose driver-side name ``key`` has ``key[12:]`` in the weight-name list runs at
+    lr * 0.1.  Under (apex) DDP ``key`` is ``"module." + name``."""
+    want = set(bert_weight_names)
+    out = {}
+    for n in names:
+        key = ("module." + n) if ddp else n
+        if key[12:] in want:
+            out[n] = mult
+    return out
+
+
+def objective1_labels(batch):
+    """objective == 1 (train_concap_struc.py:481-494): items whose text / PV / image were replaced
+    (is_next + is_next_pv_v + is_next_pv_t != 0) lose their masked-LM and region labels; the rewrite
+    multiplies by the keep flag and maps every 0 to -1 (a label id 0 too, as the reference)."""
+    keep = ((batch["is_next"] + batch["is_next_pv_v"] + batch["is_next_pv_t"]) == 0).long().unsqueeze(1)
+    out = dict(batch)
+    for k in ("image_label", "lm_label_ids", "lm_label_ids_pv"):
+        v = batch[k] * keep
+        out[k] = torch.where(v == 0, torch.full_like(v, -1), v)
+    out.pop("_label_counts", None)
+    return out
 
 
 def init_reference(fp, cfg, seed):
@@ -37,11 +89,74 @@ def init_reference(fp, cfg, seed):
     fp.shadow_fresh = False
 
 
+def optimizer_runs(fp, weight_decay=0.01, lr_mult=None, frozen_names=()):
+    """[(offset, length, wd, lr_mult)] over the flat buffer: maximal runs of adjacent optimised
+    tensors with equal (weight decay, multiplier).  Lengths are rounded up to 4 floats (16 B): the
+    alignment padding between tensors is zero in p, g, m and v and stays zero under the update."""
+    lr_mult = lr_mult or {}
+    frozen_names = set(frozen_names)
+    items = []
+    for name, shape in fp.spec:
+        seg = segment_of(name)
+        if seg == "frozen" or name in frozen_names:
+            continue
+        o = fp.offsets[name]
+        n = math.prod(shape)
+        items.append((o, o + n, weight_decay if seg == "decay" else 0.0, float(lr_mult.get(name, 1.0))))
+    items.sort()
+    runs = []
+    for a, b, wd, mu in items:
+        if runs and runs[-1][2] == wd and runs[-1][3] == mu and a - runs[-1][1] < 4:
+            runs[-1][1] = b
+        else:
+            runs.append([a, b, wd, mu])
+    return [(a, (b - a + 3) // 4 * 4, wd, mu) for a, b, wd, mu in runs]
+
+
+class LossWatch(object):
+    """Asynchronous NaN / inf fail-fast: the loss of each step is copied into pinned host memory
+    behind an event; the copy is inspected once the event has completed (a later step), so the
+    check never stalls the launch queue.  ``flush()`` (a sync) checks everything outstanding."""
+
+    def __init__(self, lag=2):
+        self.pending = collections.deque()
+        self.lag = lag
+
+    def push(self, step, loss):
+        if not loss.is_cuda:
+            v = float(loss.reshape(-1)[0])
+            if not math.isfinite(v):
+                raise FloatingPointError("non-finite loss %r at step %d" % (v, step))
+            return
+        host = torch.empty((1,), dtype=torch.float32, pin_memory=True)
+        host.copy_(loss.detach().reshape(-1)[:1], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pending.append((step, host, ev))
+        self.poll()
+
+    def poll(self, force=False):
+        while self.pending and (force or len(self.pending) > self.lag or self.pending[0][2].query()):
+            step, host, ev = self.pending.popleft()
+            ev.synchronize()
+            v = float(host[0])
+            if not math.isfinite(v):
+                self.pending.clear()
+                raise FloatingPointError("non-finite loss %r at step %d (fail-fast, SURVEY §5)" % (v, step))
+
+    def flush(self):
+        self.poll(force=True)
+
+
 class Trainer(object):
-    ADAMW = "k3m_adamw"   # pytorch_transformers AdamW (train_concap_struc.py:436-441)
+    ADAMW = None   # None: k3m_adamw_ex (pytorch_transformers AdamW / apex FusedAdam); else a legacy entry point
 
     def __init__(self, cfg, device, lr=1e-4, warmup_steps=0, total_steps=10000, seed=1234, ddp=None,
-                 loss_img_weight=1.0, beta1=0.9, beta2=0.98, eps=1e-8, weight_decay=0.01, init=True, dtype="fp32"):
+                 loss_img_weight=1.0, beta1=0.9, beta2=None, eps=1e-8, weight_decay=0.01, init=True, dtype="fp32",
+                 optimizer="adamw", lr_schedule="warmup_linear", warmup_proportion=None, accum_steps=1,
+                 lr_mult=None, frozen_names=(), objective=2, nan_check=True):
+        assert optimizer in ("adamw", "fused_adam")
+        assert lr_schedule in ("warmup_linear", "warmup_linear_fp16")
         self.engine = K3MEngine(cfg, device, seed=seed, dtype=dtype)
         fp = self.engine.fp
         if init:
@@ -50,38 +165,71 @@ class Trainer(object):
             ddp.broadcast_params(fp)
         self.ddp = ddp
         self.lr, self.warmup, self.t_total = lr, warmup_steps, total_steps
+        self.warmup_proportion = (warmup_proportion if warmup_proportion is not None
+                                  else float(warmup_steps) / max(1, total_steps))
+        self.optimizer, self.lr_schedule = optimizer, lr_schedule
+        if beta2 is None:   # pytorch_transformers AdamW (0.9, 0.98) as passed by the driver; FusedAdam default
+            beta2 = 0.98 if optimizer == "adamw" else 0.999
         self.beta1, self.beta2, self.eps, self.wd = beta1, beta2, eps, weight_decay
         self.loss_img_weight = loss_img_weight
+        self.accum_steps = int(accum_steps)
+        assert self.accum_steps >= 1
+        self.objective = objective
         self.global_step = 0
-        d0, d1 = fp.segments["decay"]
-        n0, n1 = fp.segments["no_decay"]
-        # segment lengths rounded up to 16 B: the padding between tensors is zero in p, g, m and v
-        self.segs = [(d0, (d1 - d0 + 3) // 4 * 4, weight_decay), (n0, (n1 - n0 + 3) // 4 * 4, 0.0)]
-        nopt = n0 + self.segs[1][1]
-        assert nopt <= fp.segments["frozen"][0]
+        self.micro = 0
+        if lr_schedule == "warmup_linear_fp16" and lr_mult:
+            raise NotImplementedError("the --fp16 schedule quirk is defined for the two-group optimizer only")
+        self.runs = optimizer_runs(fp, weight_decay, lr_mult, frozen_names)
+        self.excluded = sorted(set(frozen_names))
+        nopt = max(a + n for a, n, _, _ in self.runs)
+        assert nopt <= fp.segments["frozen"][0] + 4
         self.m = torch.zeros(nopt, dtype=torch.float32, device=fp.device)
         self.v = torch.zeros(nopt, dtype=torch.float32, device=fp.device)
+        self.watch = LossWatch() if nan_check else None
 
+    # ---------------------------------------------------------------- schedule
     def current_lr(self):
+        """lr of the next optimizer step for a multiplier-1 tensor of the first group."""
+        if self.lr_schedule == "warmup_linear_fp16" and self.global_step > 0:
+            return self.lr * warmup_linear_fp16(self.global_step / self.t_total, self.warmup_proportion)
+        # LambdaLR: the constructor sets lr * lambda(0); scheduler.step() after each optimizer step
         return self.lr * warmup_linear_lambda(self.global_step, self.warmup, self.t_total)
 
-    def optimizer_step(self, grad_scale=1.0):
+    def run_lr(self, wd, mult):
+        if self.lr_schedule == "warmup_linear_fp16" and wd == 0.0:
+            # only param_groups[0] (the decay group) is re-set (:584); the others keep lr * lambda(0)
+            return mult * self.lr * warmup_linear_lambda(0, self.warmup, self.t_total)
+        return mult * self.current_lr()
+
+    # ---------------------------------------------------------------- optimizer
+    def optimizer_step(self, grad_scale=1.0, zero_grad=True):
+        """One optimizer step over every run; the gradient buffer is zeroed in the same sweep."""
         fp = self.engine.fp
-        lr = self.current_lr()
         step = self.global_step + 1
         fresh = fp.shadow_fresh
-        for off, n, wd in self.segs:
+        flags = (L.ADAM_ZERO_GRAD if zero_grad else 0) | (L.ADAM_APEX if self.optimizer == "fused_adam" else 0)
+        for off, n, wd, mult in self.runs:
             if n == 0:
                 continue
             # with a bf16 encoder the same launch refreshes the weight shadow from the new fp32 values
             sh = fp.data16[off:].data_ptr() if fp.data16 is not None else None
-            L.call(self.ADAMW, fp.data[off:].data_ptr(), fp.grad[off:].data_ptr(), self.m[off:].data_ptr(),
-                   self.v[off:].data_ptr(), sh, n, lr, self.beta1, self.beta2, self.eps, wd, step, grad_scale,
-                   L.stream())
+            if self.ADAMW is not None:   # torch.optim.AdamW (fine-tuning); zeroing below
+                L.call(self.ADAMW, fp.data[off:].data_ptr(), fp.grad[off:].data_ptr(), self.m[off:].data_ptr(),
+                       self.v[off:].data_ptr(), sh, n, self.run_lr(wd, mult), self.beta1, self.beta2, self.eps, wd,
+                       step, grad_scale, L.stream())
+                continue
+            L.call("k3m_adamw_ex", fp.data[off:].data_ptr(), fp.grad[off:].data_ptr(), self.m[off:].data_ptr(),
+                   self.v[off:].data_ptr(), sh, n, self.run_lr(wd, mult), self.beta1, self.beta2, self.eps, wd, step,
+                   grad_scale, flags, L.stream())
+        if zero_grad and self.ADAMW is not None:
+            fp.grad.zero_()
+        elif zero_grad:
+            for name in self.excluded:   # --freeze: gradients the optimizer skips are dropped as well
+                fp.g[name].zero_()
         fp.shadow_fresh = fresh   # frozen tensors are not updated: the shadow stays as fresh as it was
-        fp.grad.zero_()
         self.global_step += 1
 
+    # ---------------------------------------------------------------- checkpoints
     def save_checkpoint(self, tar_path=None, bin_path=None):
         """The reference driver's .tar / .bin files (train_concap_struc.py:691-705; k3m_amd/checkpoint.py)."""
         from .checkpoint import save_checkpoint
@@ -92,18 +240,33 @@ class Trainer(object):
         from .checkpoint import load_checkpoint
         return load_checkpoint(self, tar_path)
 
+    # ---------------------------------------------------------------- the step
     def step(self, batch, noise=None, ent_neg=None, val_neg=None):
+        """One micro-step (forward + backward); the optimizer runs every ``accum_steps`` calls.
+        Returns the forward's outputs; ``out["loss"]`` is the optimised objective."""
         eng = self.engine
+        if self.objective == 1:
+            batch = objective1_labels(batch)
         out, ctx = eng.forward(batch, train=True, noise=noise, ent_neg=ent_neg, val_neg=val_neg,
-                               seed=self.global_step)
-        hook = self.ddp.grad_ready if self.ddp is not None else None
-        if self.ddp is not None:
+                               seed=self.global_step * self.accum_steps + self.micro)
+        w = 1.0 / self.accum_steps
+        out["loss"] = out["masked_lm_loss"] + out["masked_lm_loss_pv"] + out["loss_lpm"] + \
+            out["masked_img_loss"] * self.loss_img_weight
+        last = self.micro + 1 == self.accum_steps
+        sync = self.ddp is not None and last
+        if sync:
             self.ddp.begin(eng)
-        eng.backward(ctx, w_mlm=1.0, w_img=self.loss_img_weight, w_lpm=1.0, grad_ready=hook)
-        scale = 1.0
-        if self.ddp is not None:
-            self.ddp.finish()
-            scale = 1.0 / self.ddp.world
-        self.optimizer_step(grad_scale=scale)
-        eng.step_count += 1
+        eng.backward(ctx, w_mlm=w, w_img=self.loss_img_weight * w, w_lpm=w,
+                     grad_ready=self.ddp.grad_ready if sync else None)
+        if self.watch is not None:
+            self.watch.push(self.global_step, out["loss"])
+        self.micro += 1
+        if last:
+            scale = 1.0
+            if sync:
+                self.ddp.finish()
+                scale = 1.0 / self.ddp.world
+            self.optimizer_step(grad_scale=scale)
+            self.micro = 0
+            eng.step_count += 1
         return out

@@ -53,11 +53,11 @@ class _Step(torch.autograd.Function):
 class BertForMultiModalPreTraining_tri_stru(nn.Module):
     """Same constructor / forward contract as the reference class (vilbert_k3m.py:2186)."""
 
-    def __init__(self, config, device=None, seed=42):
+    def __init__(self, config, device=None, seed=42, dtype="fp32"):
         super().__init__()
         self.config = config
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-        self.engine = K3MEngine(config, dev, seed=seed)
+        self.engine = K3MEngine(config, dev, seed=seed, dtype=dtype)
         init_reference(self.engine.fp, config, seed)
         self._names = [n for n, _ in self.engine.fp.spec]
         for n in self._names:
@@ -151,6 +151,11 @@ class BertForMultiModalPreTraining_tri_stru(nn.Module):
         B, R = batch["image_feat"].shape[:2]
         batch["image_mask"] = (d(image_attention_mask) if image_attention_mask is not None
                                else torch.ones((B, R), dtype=torch.int64, device=dev))
+        # labelled-row counts attached by the loaders (k3m_amd/loaders.py): no device->host sync
+        n_m = getattr(masked_lm_labels, "_k3m_n_labels", None)
+        n_v = getattr(image_label, "_k3m_n_labels", None)
+        if n_m is not None and n_v is not None:
+            batch["_label_counts"] = (n_m, n_v)
         kw = {"noise": gumbel_noise, "ent_neg": ent_neg, "val_neg": val_neg}
         mlm_t, img, mlm_pv, nsp, c_init, c_final, lpm = _Step.apply(self._anchor, self, batch, kw)
         return (mlm_t, img, 0, mlm_pv, 0, 0, nsp, c_init, c_final, lpm)

@@ -358,3 +358,17 @@ def adamw_step(p, g, m, v, step, lr, wd, beta1=0.9, beta2=0.98, eps=1e-8):
     p.addcdiv_(m, denom, value=-step_size)
     if wd > 0.0:
         p.add_(p, alpha=-lr * wd)
+
+
+def fused_adam_step(p, g, m, v, step, lr, wd, beta1=0.9, beta2=0.999, eps=1e-8, bias_correction=False):
+    """apex FusedAdam, adam_w_mode (the optimizer of the mixed-precision driver branches,
+    train_concap_struc.py:410-411, :426: bias_correction=False; per-group weight_decay 0.01 / 0.0
+    overrides the constructor's 5e-4).  Restated from apex's multi_tensor_adam (ADAM_MODE_1):
+    p -= lr * ((m / bc1) / (sqrt(v / bc2) + eps) + wd * p).  Unpinned: apex is not installed."""
+    m.mul_(beta1).add_(g, alpha=1.0 - beta1)
+    v.mul_(beta2).addcmul_(g, g, value=1.0 - beta2)
+    bc1 = 1.0 - beta1 ** step if bias_correction else 1.0
+    bc2 = 1.0 - beta2 ** step if bias_correction else 1.0
+    denom = (v / bc2).sqrt().add_(eps)
+    upd = (m / bc1) / denom + wd * p
+    p.sub_(lr * upd)

@@ -23,7 +23,11 @@ for s in "$@"; do
     lab) step lab 300 scripts/lab/gemm_lab 10 ;;
     smoke) step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
     parity) step parity 900 python -m pytest tests/test_gpu_parity.py -x -q ;;
-    gpu) step gputests 1200 python -m pytest tests -m gpu -q ;;
+    gpu) step gputests 1200 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ;;
+    bench3) step bench3 600 python bench.py --config 3 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    bench4) step bench4 900 python bench.py --config 4 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    bench5) step bench5 900 python bench.py --config 5 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    spawn2) step spawn2 600 python bench.py --gpus 2 --steps 3 --warmup 1 --backend gloo --batch 16 ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
     benchq) step bench 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     profbf) export TMPDIR=/tmp; step profbf 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profbf -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --dtype bf16 ;;
