@@ -140,4 +140,32 @@ __device__ __forceinline__ float dgelu_f(float x) {
 }
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// erf-GELU and its derivative with a short erfc (Abramowitz & Stegun 7.1.26: |erf error| <= 1.5e-7,
+// i.e. Phi(x) to ~7.5e-8 absolute): one v_rcp, one v_exp, five FMAs shared by GELU and dGELU.
+// Used by the bf16 GEMM epilogues, whose outputs round to 8 significant bits (the exact-erff forms
+// above cost ~3x the VALU and serialised the epilogue of the output-heavy FFN GEMMs).
+__device__ __forceinline__ void phi_fast(float x, float& Phi, float& pdf) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float poly = fmaf(1.061405429f, t, -1.453152027f);
+  poly = fmaf(poly, t, 1.421413741f);
+  poly = fmaf(poly, t, -0.284496736f);
+  poly = fmaf(poly, t, 0.254829592f);
+  poly *= t;
+  const float e = __expf(-z * z);                 // exp(-x^2 / 2)
+  const float half_erfc = 0.5f * poly * e;        // 0.5 * erfc(|x| / sqrt 2)
+  Phi = x >= 0.f ? 1.0f - half_erfc : half_erfc;
+  pdf = 0.3989422804014327f * e;
+}
+__device__ __forceinline__ float gelu_fast(float x) {
+  float P, d;
+  phi_fast(x, P, d);
+  return x * P;
+}
+__device__ __forceinline__ float dgelu_fast(float x) {
+  float P, d;
+  phi_fast(x, P, d);
+  return fmaf(x, d, P);
+}
+
 static inline int k3m_cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }

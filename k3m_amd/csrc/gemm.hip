@@ -136,6 +136,7 @@ bool prefer_256x256(const K3mGemm& g) {
 }  // namespace
 
 int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st);  // gemm_bf16.hip
+int k3m_gemm_bf16_grouped_impl(const K3mGemm* gs, int count, hipStream_t st, bool* handled);
 
 extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
   if (!gp) return K3M_EINVAL;
@@ -222,6 +223,11 @@ extern "C" int k3m_gemm_grouped(const K3mGemm* gs, int count, hipStream_t st) {
   if (count == 0) return 0;
   // one template for the whole group: same layout, epilogue, dtype, algorithm, 16-B aligned operands
   const K3mGemm& g0 = gs[0];
+  if (g0.dtype == K3M_BF16) {   // bf16 encoder: the large-tile grouped kernel (gemm_bf16.hip) when eligible
+    bool handled = false;
+    const int r = k3m_gemm_bf16_grouped_impl(gs, count, st, &handled);
+    if (handled || r) return r;
+  }
   bool same = g0.dtype == K3M_F32 && g0.c_dtype == K3M_F32 && g0.f32_algo == K3M_F32_SPLIT_BF16X6;
   k3m_x6::GemmGroup grp = {};
   int nb = 0, live = 0;

@@ -1,0 +1,439 @@
+// Large-tile bf16 GEMM for gfx950 (the bf16 encoder of the mixed-precision step, configs 3-5):
+// bf16 operands, fp32 accumulation, fp32 or bf16 C with the fused epilogues of k3m_gemm.
+//
+// Structure (MI355X_MICROARCH.md / cdna_hip_programming.md §5):
+//  * block tile TBM x TBN x 64 (256x256 or 256x128), 8 waves of 512 threads, one block per CU,
+//    each wave a (TBM/WM) x (TBN/WN) slab of v_mfma_f32_16x16x32_bf16 tiles (the 16x16x32 shape
+//    holds a higher clock than 32x32x16 on random data at equal cycles per FLOP);
+//  * operands go global -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction):
+//    no staging registers, no VALU, no ds_write; two LDS stages, the next k-tile's DMA in flight
+//    while the current one feeds the MFMAs, one vmcnt(0) + barrier per k-tile;
+//  * LDS images are lane-linear per DMA instruction, so the bank-conflict swizzles live in the
+//    per-lane SOURCE address and the fragment read applies the same XOR (an involution):
+//      K-contiguous operand: [TILE][64] bf16, chunk c of row r at slot c ^ ((r >> 1) & 7)
+//        (fragments by ds_read_b128, conflict-free for the 16-lane read groups);
+//      MN-contiguous operand (W in input gradients, dY^T and X in weight gradients): [64][TILE],
+//        chunk ch of k-row k at slot ch ^ (((k & 3) << 2) | ((k >> 2) & 3)), fragments by the
+//        transposing ds_read_b64_tr_b16 (no register transpose);
+//  * edge rows / columns: source addresses clamped into the operand (their products reach only C
+//    entries the epilogue does not store); K must be a multiple of 64 (callers fall back otherwise);
+//  * XCD-aware bijective block remap, 8 row-tiles walking N together;
+//  * epilogue through LDS: row-contiguous 16-B stores, bias / bias+GELU (+pre-activation) / dGELU /
+//    bias+sigmoid / alpha, beta; split-K writes raw fp32 slabs reduced by the caller.
+#pragma once
+#include "common.h"
+
+namespace k3m_b16 {
+
+constexpr int BK = 64;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef short short8v __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) short4v lds_short4v;
+
+__device__ __forceinline__ int kc_off(int r, int c) { return r * BK + ((c ^ ((r >> 1) & 7)) << 3); }
+template <int TILE>
+__device__ __forceinline__ int mn_off(int k, int ch) {
+  return k * TILE + ((ch ^ (((k & 3) << 2) | ((k >> 2) & 3))) << 3);
+}
+
+__device__ __forceinline__ void glds16(const uint16_t* g, uint16_t* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+// LDS-DMA sources of one operand tile (TILE rows/columns x 64 k): a wave-uniform (SGPR) running base
+// that advances by one k-tile per issue, plus per-lane 32-bit element offsets (the instruction's
+// saddr + voffset form: no 64-bit per-lane pointers to keep or advance).  Callers guarantee the
+// offsets fit (k3m_gemm_bf16_impl checks the operand extents).
+template <bool KC, int TILE, int NT>
+struct Loader {
+  static constexpr int INSTS = TILE * BK * 2 / 1024;   // wave instructions per k-tile
+  static constexpr int NW = NT / 64;
+  static constexpr int NI = INSTS / NW;                 // per wave
+  static_assert(INSTS % NW == 0, "tile must split evenly over the waves");
+  const uint16_t* base;   // wave-uniform
+  long long step;         // elements per k-tile
+  uint32_t off[NI];
+  int lds0;               // wave-uniform element offset of the wave's first instruction in the image
+
+  __device__ __forceinline__ void init(const uint16_t* __restrict__ a, long long ld, int mn0, int kbeg, int MN) {
+    const int l = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    lds0 = w * 512;
+    base = a + (KC ? (long long)kbeg : (long long)kbeg * ld);
+    step = KC ? BK : BK * ld;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int inst = w + NW * i;
+      if constexpr (KC) {
+        const int row = inst * 8 + (l >> 3), slot = l & 7;
+        const int ch = slot ^ ((row >> 1) & 7);
+        off[i] = (uint32_t)((long long)min(mn0 + row, MN - 1) * ld + ch * 8);
+      } else {
+        constexpr int CPR = TILE / 8, RPI = 64 / CPR;   // 16-B chunks per k-row, k-rows per instruction
+        const int kr = inst * RPI + l / CPR, slot = l % CPR;
+        const int ch = slot ^ (((kr & 3) << 2) | ((kr >> 2) & 3));
+        off[i] = (uint32_t)((long long)kr * ld + max(0, min(mn0 + ch * 8, MN - 8)));
+      }
+    }
+  }
+  __device__ __forceinline__ void issue(uint16_t* img) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) glds16(base + off[i], img + lds0 + i * NW * 512);
+    base += step;
+  }
+};
+
+// 16x16x32 operand fragment: lane l gets X[mnb + (l & 15)][32 s + 8 (l >> 4) + e], e = 0..7
+template <bool KC, int TILE>
+__device__ __forceinline__ bf16x8 frag(const uint16_t* img, int mnb, int s, int lane) {
+  if constexpr (KC) {
+    return *reinterpret_cast<const bf16x8*>(img + kc_off(mnb + (lane & 15), 4 * s + (lane >> 4)));
+  } else {
+    // two transposed 4(k) x 16(mn) block reads per 16-lane group g = lane >> 4: k-rows 32s + 8g + q
+    // (+4); lane 4q+p addresses row q, columns 4p..4p+3 (ds_read_b64_tr_b16)
+    const int q = (lane >> 2) & 3, p = lane & 3;
+    const int ch = (mnb >> 3) + (p >> 1);
+    const int r0 = 32 * s + 8 * (lane >> 4) + q;
+    const short4v x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(img + mn_off<TILE>(r0, ch) + 4 * (p & 1)));
+    const short4v x1 =
+        __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(img + mn_off<TILE>(r0 + 4, ch) + 4 * (p & 1)));
+    const short8v v = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+template <int TBM, int TBN, int WM, int WN>
+struct Shape {
+  static constexpr int NT = 64 * WM * WN;
+  static constexpr int FM = TBM / WM / 16, FN = TBN / WN / 16;
+  static constexpr int STAGE = (TBM + TBN) * BK;          // bf16 elements per stage
+  static constexpr int LDS = 2 * STAGE;                   // bf16 elements
+};
+
+template <bool AK, bool BK_, int TBM, int TBN, int FM, int FN>
+__device__ __forceinline__ void read_frags(const uint16_t* stage, int wm, int wn, int s, int lane, bf16x8 (&a)[FM],
+                                           bf16x8 (&b)[FN]) {
+#pragma unroll
+  for (int i = 0; i < FM; ++i) a[i] = frag<AK, TBM>(stage, wm + 16 * i, s, lane);
+#pragma unroll
+  for (int j = 0; j < FN; ++j) b[j] = frag<BK_, TBN>(stage + TBM * BK, wn + 16 * j, s, lane);
+}
+
+template <int FM, int FN>
+__device__ __forceinline__ void mfmas(floatx4 (&acc)[FM][FN], const bf16x8 (&a)[FM], const bf16x8 (&b)[FN]) {
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+}
+
+// acc[i][j] += A[m0 + wm + 16 i .., kbeg:kend] . B[n0 + wn + 16 j .., kbeg:kend]^T;  (kend - kbeg) % 64 == 0
+//
+// Software pipeline (two LDS stages, two register fragment sets F0 / F1 = k-substeps 0 / 1 of a
+// 64-deep k-tile), per k-tile kt:
+//   read F1(kt) | MFMA F0(kt)                      (the reads of F1 fly under 32 MFMAs)
+//   wait lgkmcnt(0) vmcnt(0); barrier              (tile kt+1 landed; every read of stage kt done)
+//   DMA tile kt+2 -> stage kt & 1 | read F0(kt+1) | MFMA F1(kt)
+// so each tile's DMA has a whole tile of MFMAs (64 per wave) to land, the fragment reads of one
+// substep always overlap the MFMAs of the other, and no LDS read is in flight across a barrier
+// (the DMA that follows a barrier overwrites the stage just read).  sched_barrier pins the order.
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_>
+__device__ __forceinline__ void mainloop(const uint16_t* __restrict__ A, long long lda, const uint16_t* __restrict__ B,
+                                         long long ldb, int M, int N, int m0, int n0, int kbeg, int kend,
+                                         uint16_t* smem, floatx4 (&acc)[TBM / WM / 16][TBN / WN / 16]) {
+  using S = Shape<TBM, TBN, WM, WN>;
+  constexpr int FM = S::FM, FN = S::FN;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = (w / WN) * (TBM / WM), wn = (w % WN) * (TBN / WN);
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  Loader<AK, TBM, S::NT> la;
+  Loader<BK_, TBN, S::NT> lb;
+  la.init(A, lda, m0, kbeg, M);
+  lb.init(B, ldb, n0, kbeg, N);
+  const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
+  if (nk == 0) return;
+  la.issue(smem);
+  lb.issue(smem + TBM * BK);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (nk > 1) {
+    la.issue(smem + S::STAGE);
+    lb.issue(smem + S::STAGE + TBM * BK);
+  }
+  bf16x8 a0[FM], b0[FN], a1[FM], b1[FN];
+  read_frags<AK, BK_, TBM, TBN, FM, FN>(smem, wm, wn, 0, lane, a0, b0);
+  for (int kt = 0; kt < nk; ++kt) {
+    uint16_t* cur = smem + (kt & 1) * S::STAGE;
+    uint16_t* nxt = smem + ((kt + 1) & 1) * S::STAGE;
+    read_frags<AK, BK_, TBM, TBN, FM, FN>(cur, wm, wn, 1, lane, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    mfmas<FM, FN>(acc, a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 2 < nk) {
+      la.issue(cur);
+      lb.issue(cur + TBM * BK);
+    }
+    // unconditional (past the last tile it reads a stale stage nobody uses): a branch here would
+    // make the wait before MFMA F0 a conservative lgkmcnt(0) instead of a counted one
+    read_frags<AK, BK_, TBM, TBN, FM, FN>(nxt, wm, wn, 0, lane, a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    mfmas<FM, FN>(acc, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();   // the epilogue reuses the stages
+}
+
+__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
+  const floatx4 a = *reinterpret_cast<const floatx4*>(p), b = *reinterpret_cast<const floatx4*>(p + 4);
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+__device__ __forceinline__ void load8(const bf16_t* p, float (&v)[8]) {
+  const u32x4 a = *reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[2 * q] = __uint_as_float(a[q] << 16);
+    v[2 * q + 1] = __uint_as_float(a[q] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
+  *reinterpret_cast<floatx4*>(p) = floatx4{v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<floatx4*>(p + 4) = floatx4{v[4], v[5], v[6], v[7]};
+}
+__device__ __forceinline__ void store8(bf16_t* p, const float (&v)[8]) {
+  u32x4 a;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) a[q] = (uint32_t)from_f<bf16_t>(v[2 * q]).x | ((uint32_t)from_f<bf16_t>(v[2 * q + 1]).x << 16);
+  *reinterpret_cast<u32x4*>(p) = a;
+}
+
+// 8 consecutive C / aux elements as raw registers (prefetched before they are needed)
+template <typename CT> struct Raw8;
+template <> struct Raw8<bf16_t> {
+  u32x4 r;
+  __device__ __forceinline__ void load(const bf16_t* p) { r = *reinterpret_cast<const u32x4*>(p); }
+  __device__ __forceinline__ void get(float (&v)[8]) const {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[2 * q] = __uint_as_float(r[q] << 16);
+      v[2 * q + 1] = __uint_as_float(r[q] & 0xffff0000u);
+    }
+  }
+};
+template <> struct Raw8<float> {
+  floatx4 a, b;
+  __device__ __forceinline__ void load(const float* p) {
+    a = *reinterpret_cast<const floatx4*>(p);
+    b = *reinterpret_cast<const floatx4*>(p + 4);
+  }
+  __device__ __forceinline__ void get(float (&v)[8]) const {
+    v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+  }
+};
+
+// Epilogue through LDS (the stages are free after the main loop): per pass each wave stages 32 rows
+// x (TBN/WN) columns of its fp32 accumulators (row stride TBN/WN + 8 floats), then every lane
+// handles 8 consecutive columns of one row: epilogue math, 16-B (bf16) / 32-B (fp32) stores.
+// The C (beta) / aux (dGELU) values it reads are loaded ahead: two 32-row groups in flight for bf16
+// C, one for fp32 C (register budget) — a load issued right before its use exposed a full HBM latency
+// per row group and made the output-heavy epilogues latency-bound.
+// 16x16 accumulator layout: acc[i][j][r] = C[wm + 16 i + 4 (lane >> 4) + r][wn + 16 j + (lane & 15)].
+template <int TBM, int TBN, int WM, int WN, int EPI, typename CT>
+__device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint16_t* smem_u16,
+                                         floatx4 (&acc)[TBM / WM / 16][TBN / WN / 16], int slice) {
+  using S = Shape<TBM, TBN, WM, WN>;
+  constexpr int FM = S::FM, FN = S::FN;
+  constexpr int WNC = TBN / WN, WS = WNC + 8, LPR = WNC / 8, RPP = 64 / LPR, NPS = 32 / RPP, NG = FM / 2;
+  static_assert(S::NT / 64 * 32 * WS * 4 <= S::LDS * 2, "epilogue staging exceeds the LDS stages");
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = (w / WN) * (TBM / WM), wn = (w % WN) * WNC;
+  float* wl = reinterpret_cast<float*>(smem_u16) + w * 32 * WS;
+  const int M = g.m, N = g.n;
+  const bool split = g.splitk > 1;
+  CT* C = split ? reinterpret_cast<CT*>(g.ws + (long long)slice * M * N) : static_cast<CT*>(g.c);
+  const long long ldc = split ? N : g.ldc;
+  const float alpha = split ? 1.f : g.alpha, beta = split ? 0.f : g.beta;
+  CT* aux = static_cast<CT*>(g.aux);
+  const float* bias = g.bias;
+  constexpr bool HAS_AUX = EPI == K3M_EPI_BIAS_GELU || EPI == K3M_EPI_DGELU;
+  constexpr bool HAS_BIAS = EPI == K3M_EPI_BIAS || EPI == K3M_EPI_BIAS_GELU || EPI == K3M_EPI_BIAS_SIGMOID;
+  constexpr bool CAN_OLD = EPI == K3M_EPI_NONE || EPI == K3M_EPI_BIAS || EPI == K3M_EPI_DGELU;
+  const bool cvec = (ldc % 8 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) &&
+                    (!HAS_AUX || ((g.ldaux % 8 == 0) && ((reinterpret_cast<uintptr_t>(aux) & 15) == 0)));
+  const int lr = lane / LPR, lc = (lane % LPR) * 8;
+  const int col = n0 + wn + lc;
+  float bb[8];
+  if constexpr (HAS_BIAS) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bb[e] = col + e < N ? bias[col + e] : 0.f;
+  }
+  const bool rd_old = CAN_OLD && beta != 0.f;
+  // prefetch ring: PD row groups of (dGELU aux | old C) values ahead
+  constexpr bool PRE = EPI == K3M_EPI_DGELU || CAN_OLD;
+  constexpr int PD = (sizeof(CT) == 2 && NG >= 2) ? 2 : 1;   // groups in flight (register budget)
+  Raw8<CT> pax[PRE && EPI == K3M_EPI_DGELU ? PD : 1][NPS], pold[PRE ? PD : 1][NPS];
+  auto row_of = [&](int i2, int ps) { return m0 + wm + 16 * i2 + ps * RPP + lr; };
+  auto prefetch = [&](int grp, int slot) {
+#pragma unroll
+    for (int ps = 0; ps < NPS; ++ps) {
+      const int row = row_of(2 * grp, ps);
+      if (row < M && cvec && col + 8 <= N) {
+        if constexpr (EPI == K3M_EPI_DGELU) pax[slot][ps].load(aux + (long long)row * g.ldaux + col);
+        if constexpr (CAN_OLD) {
+          if (rd_old) pold[slot][ps].load(C + (long long)row * ldc + col);
+        }
+      }
+    }
+  };
+  if constexpr (PRE) {
+#pragma unroll
+    for (int q = 0; q < PD; ++q) prefetch(q, q);
+  }
+#pragma unroll
+  for (int grp = 0; grp < NG; ++grp) {
+    const int i2 = 2 * grp;
+    const int slot = grp % PD;
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wl[(16 * ii + 4 * (lane >> 4) + r) * WS + 16 * j + (lane & 15)] = acc[i2 + ii][j][r];
+    __syncthreads();
+#pragma unroll
+    for (int ps = 0; ps < NPS; ++ps) {
+      const int rr = ps * RPP + lr;
+      const int row = row_of(i2, ps);
+      const floatx4 v0 = *reinterpret_cast<const floatx4*>(wl + rr * WS + lc);
+      const floatx4 v1 = *reinterpret_cast<const floatx4*>(wl + rr * WS + lc + 4);
+      if (row >= M || col >= N) continue;
+      float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      const bool full = cvec && col + 8 <= N;
+      CT* cp = C + (long long)row * ldc + col;
+      CT* ap = HAS_AUX ? aux + (long long)row * g.ldaux + col : nullptr;
+      float old[8], ax[8];
+      if constexpr (EPI == K3M_EPI_DGELU) {
+        if (full) pax[slot][ps].get(ax);
+        else
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ax[e] = col + e < N ? to_f(ap[e]) : 0.f;
+      }
+      if (rd_old) {
+        if (full) pold[slot][ps].get(old);
+        else
+#pragma unroll
+          for (int e = 0; e < 8; ++e) old[e] = col + e < N ? to_f(cp[e]) : 0.f;
+      }
+      float o[8], pa[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if constexpr (EPI == K3M_EPI_NONE) {
+          o[e] = alpha * v[e];
+        } else if constexpr (EPI == K3M_EPI_BIAS) {
+          o[e] = alpha * (v[e] + bb[e]);
+        } else if constexpr (EPI == K3M_EPI_BIAS_GELU) {
+          pa[e] = v[e] + bb[e];
+          o[e] = gelu_fast(to_f(from_f<CT>(pa[e])));  // gelu of the stored pre-activation the backward sees
+        } else if constexpr (EPI == K3M_EPI_DGELU) {
+          o[e] = alpha * v[e] * dgelu_fast(ax[e]);
+        } else {
+          o[e] = sigmoid_f(v[e] + bb[e]);
+        }
+        if (rd_old) o[e] = fmaf(beta, old[e], o[e]);
+      }
+      if (full) {
+        store8(cp, o);
+        if constexpr (EPI == K3M_EPI_BIAS_GELU) store8(ap, pa);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (col + e < N) {
+            cp[e] = from_f<CT>(o[e]);
+            if constexpr (EPI == K3M_EPI_BIAS_GELU) ap[e] = from_f<CT>(pa[e]);
+          }
+      }
+    }
+    if constexpr (PRE) {
+      if (grp + PD < NG) prefetch(grp + PD, slot);   // refill the slot just consumed
+    }
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ int xcd_remap(int id, int nblk) {
+  const int xcd = id & 7, q = nblk >> 3, rr = nblk & 7;
+  const int base = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
+  return base + (id >> 3);
+}
+
+// tile (m0, n0) and split slice of block `id` of one problem (8 row-tiles walk N together)
+__device__ __forceinline__ void coords(int local, int M, int N, int TBM, int TBN, int& m0, int& n0, int& slice) {
+  const int tm = (M + TBM - 1) / TBM, tn = (N + TBN - 1) / TBN, tiles = tm * tn;
+  slice = local / tiles;
+  const int t = local - slice * tiles;
+  constexpr int GROUP = 8;
+  const int group_sz = GROUP * tn, first_m = (t / group_sz) * GROUP, gm_sz = min(tm - first_m, GROUP);
+  m0 = (first_m + (t % group_sz) % gm_sz) * TBM;
+  n0 = ((t % group_sz) / gm_sz) * TBN;
+}
+
+__device__ __forceinline__ void k_range(const K3mGemm& g, int slice, int& kbeg, int& kend) {
+  kbeg = 0;
+  kend = g.k;
+  if (g.splitk > 1) {
+    const int per = ((g.k + g.splitk - 1) / g.splitk + BK - 1) / BK * BK;
+    kbeg = slice * per;
+    kend = min(g.k, kbeg + per);
+  }
+}
+
+constexpr int GROUP_MAX = 8;
+struct GemmGroup {
+  K3mGemm g[GROUP_MAX];
+  int start[GROUP_MAX + 1];
+  int count;
+};
+
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT>
+__global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(K3mGemm g) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[Shape<TBM, TBN, WM, WN>::LDS];
+  const int tm = (g.m + TBM - 1) / TBM, tn = (g.n + TBN - 1) / TBN;
+  const int nsl = g.splitk > 1 ? g.splitk : 1;
+  const int id = xcd_remap(blockIdx.x, tm * tn * nsl);
+  int m0, n0, slice, kbeg, kend;
+  coords(id, g.m, g.n, TBM, TBN, m0, n0, slice);
+  k_range(g, slice, kbeg, kend);
+  floatx4 acc[TBM / WM / 16][TBN / WN / 16];
+  mainloop<TBM, TBN, WM, WN, AK, BK_>(static_cast<const uint16_t*>(g.a), g.lda, static_cast<const uint16_t*>(g.b),
+                                      g.ldb, g.m, g.n, m0, n0, kbeg, kend, smem, acc);
+  epilogue<TBM, TBN, WM, WN, EPI, CT>(g, m0, n0, smem, acc, slice);
+}
+
+// several independent problems sharing the template in one grid: blocks [start[p], start[p+1]) are
+// problem p (split-major: slice, tile)
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT>
+__global__ __launch_bounds__(64 * WM * WN, 1) void gemm_grouped_kernel(GemmGroup grp) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[Shape<TBM, TBN, WM, WN>::LDS];
+  const int id = xcd_remap(blockIdx.x, grp.start[grp.count]);
+  int p = 0;
+  while (p + 1 < grp.count && id >= grp.start[p + 1]) ++p;
+  const K3mGemm& g = grp.g[p];
+  int m0, n0, slice, kbeg, kend;
+  coords(id - grp.start[p], g.m, g.n, TBM, TBN, m0, n0, slice);
+  k_range(g, slice, kbeg, kend);
+  floatx4 acc[TBM / WM / 16][TBN / WN / 16];
+  mainloop<TBM, TBN, WM, WN, AK, BK_>(static_cast<const uint16_t*>(g.a), g.lda, static_cast<const uint16_t*>(g.b),
+                                      g.ldb, g.m, g.n, m0, n0, kbeg, kend, smem, acc);
+  epilogue<TBM, TBN, WM, WN, EPI, CT>(g, m0, n0, smem, acc, slice);
+}
+
+}  // namespace k3m_b16

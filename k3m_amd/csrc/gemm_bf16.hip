@@ -16,7 +16,10 @@
 //     loads a 4(k) x 8(mn) block as four 16-B row pieces, transposes it in registers (16-bit
 //     permutes) and writes eight 8-B k-runs (ds_write_b64) into the same K-contiguous image.
 // Split-K writes fp32 slabs, reduced deterministically by a second kernel (weight gradients).
+#include <cstdlib>
+
 #include "common.h"
+#include "gemm_b16_tile.h"
 
 namespace {
 
@@ -283,6 +286,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(K3mGemm g) {
       store_tile<AM, TBM>(smem + (cur ^ 1) * BUF, ra);
       store_tile<BM_, TBN>(smem + (cur ^ 1) * BUF + TBM * BK, rb);
     }
+    // every fragment read of this stage has returned before any wave passes the barrier and
+    // restages it (hipcc may sink the MFMAs, and with them the reads' waits, below the barrier)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
@@ -351,9 +357,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(K3mGemm g) {
           o[e] = alpha * (v[e] + bb[e]);
         } else if constexpr (EPI == K3M_EPI_BIAS_GELU) {
           pa[e] = v[e] + bb[e];
-          o[e] = gelu_f(to_f(from_f<CT>(pa[e])));  // gelu of the stored pre-activation the backward sees
+          o[e] = gelu_fast(to_f(from_f<CT>(pa[e])));  // gelu of the stored pre-activation the backward sees
         } else if constexpr (EPI == K3M_EPI_DGELU) {
-          o[e] = alpha * v[e] * dgelu_f(ax[e]);
+          o[e] = alpha * v[e] * dgelu_fast(ax[e]);
         } else {
           o[e] = sigmoid_f(v[e] + bb[e]);
         }
@@ -428,24 +434,177 @@ int launch_ct(const K3mGemm& g, bool ak, bool bk, bool vec, hipStream_t st) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-}  // namespace
-
-// Called by k3m_gemm (gemm.hip) for dtype == K3M_BF16; arguments already validated there.
-int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st) {
-  K3M_ARG(g.splitk <= 1 || g.c_dtype == K3M_F32);
+// ---------------------------------------------------------------- large-tile path (gemm_b16_tile.h)
+// Eligible: 16-B aligned operands with ld % 8 == 0, K a multiple of 64, and either both operands
+// K-contiguous (forward) or A K-contiguous / B MN-contiguous (input gradients) with any epilogue, or
+// both MN-contiguous (weight gradients) with the plain fp32 epilogue.
+bool big_ok(const K3mGemm& g, bool vec) {
+  if (!vec || g.k % k3m_b16::BK != 0 || g.k == 0) return false;
   const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
-  const bool av = aligned16(g.a) && (g.lda % 8 == 0) && ((ak ? g.k : g.m) % 8 == 0);
-  const bool bv = aligned16(g.b) && (g.ldb % 8 == 0) && ((bk ? g.k : g.n) % 8 == 0);
-  const bool vec = av && bv;
-  int rc = g.c_dtype == K3M_F32 ? launch_ct<float>(g, ak, bk, vec, st) : launch_ct<bf16_t>(g, ak, bk, vec, st);
-  if (rc) return rc;
-  K3M_CHECK_LAUNCH();
+  // weight gradients (both operands MN-contiguous: two transposing reads per fragment on both sides)
+  // measured 2x slower on this kernel than on the 128x128 register-staged one: they stay there
+  if (!ak) return false;
+  if (g.splitk > 1 && ((g.k + g.splitk - 1) / g.splitk) < k3m_b16::BK) return false;
+  return true;
+}
+
+long long nb_of(const K3mGemm& g, int bm, int bn) {
+  return (long long)((g.m + bm - 1) / bm) * ((g.n + bn - 1) / bn) * (g.splitk > 1 ? g.splitk : 1);
+}
+
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, typename CT>
+int big_launch_epi(const K3mGemm& g, hipStream_t st) {
+  const dim3 grid((unsigned)nb_of(g, TBM, TBN));
+  switch (g.epilogue) {
+#define K3M_GEMM_CASE(E)                                                                                     \
+    case E:                                                                                                  \
+      hipLaunchKernelGGL((k3m_b16::gemm_kernel<TBM, TBN, WM, WN, AK, BK_, E, CT>), grid, dim3(64 * WM * WN), 0, st, g); \
+      break;
+    K3M_GEMM_CASE(K3M_EPI_NONE)
+    K3M_GEMM_CASE(K3M_EPI_BIAS)
+    K3M_GEMM_CASE(K3M_EPI_BIAS_GELU)
+    K3M_GEMM_CASE(K3M_EPI_DGELU)
+    K3M_GEMM_CASE(K3M_EPI_BIAS_SIGMOID)
+#undef K3M_GEMM_CASE
+    default: return K3M_EINVAL;
+  }
+  return 0;
+}
+
+template <int TBM, int TBN, int WM, int WN>
+int big_launch(const K3mGemm& g, hipStream_t st) {
+  const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
+  if (!ak) {
+    if (g.epilogue != K3M_EPI_NONE) return K3M_EINVAL;
+    hipLaunchKernelGGL((k3m_b16::gemm_kernel<TBM, TBN, WM, WN, false, false, K3M_EPI_NONE, float>),
+                       dim3((unsigned)nb_of(g, TBM, TBN)), dim3(64 * WM * WN), 0, st, g);
+    return 0;
+  }
+  if (g.c_dtype == K3M_F32)
+    return bk ? big_launch_epi<TBM, TBN, WM, WN, true, true, float>(g, st)
+              : big_launch_epi<TBM, TBN, WM, WN, true, false, float>(g, st);
+  return bk ? big_launch_epi<TBM, TBN, WM, WN, true, true, bf16_t>(g, st)
+            : big_launch_epi<TBM, TBN, WM, WN, true, false, bf16_t>(g, st);
+}
+
+// tile policy: 256x256 when it still gives >= ~3/4 of a wave of blocks, else 256x128
+bool big_prefers_256(long long nb256) { return nb256 >= 192; }
+
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, typename CT>
+int big_grouped_epi(const k3m_b16::GemmGroup& grp, int epi, hipStream_t st) {
+  const dim3 grid(grp.start[grp.count]);
+  switch (epi) {
+#define K3M_GROUP_CASE(E)                                                                                      \
+    case E:                                                                                                    \
+      hipLaunchKernelGGL((k3m_b16::gemm_grouped_kernel<TBM, TBN, WM, WN, AK, BK_, E, CT>), grid, dim3(64 * WM * WN), 0, \
+                         st, grp);                                                                             \
+      break;
+    K3M_GROUP_CASE(K3M_EPI_NONE)
+    K3M_GROUP_CASE(K3M_EPI_BIAS)
+    K3M_GROUP_CASE(K3M_EPI_BIAS_GELU)
+    K3M_GROUP_CASE(K3M_EPI_DGELU)
+    K3M_GROUP_CASE(K3M_EPI_BIAS_SIGMOID)
+#undef K3M_GROUP_CASE
+    default: return K3M_EINVAL;
+  }
+  return 0;
+}
+
+template <int TBM, int TBN, int WM, int WN>
+int big_grouped(const k3m_b16::GemmGroup& grp, hipStream_t st) {
+  const K3mGemm& g = grp.g[0];
+  const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
+  if (!ak) {
+    if (g.epilogue != K3M_EPI_NONE) return K3M_EINVAL;
+    hipLaunchKernelGGL((k3m_b16::gemm_grouped_kernel<TBM, TBN, WM, WN, false, false, K3M_EPI_NONE, float>),
+                       dim3(grp.start[grp.count]), dim3(64 * WM * WN), 0, st, grp);
+    return 0;
+  }
+  if (g.c_dtype == K3M_F32)
+    return bk ? big_grouped_epi<TBM, TBN, WM, WN, true, true, float>(grp, g.epilogue, st)
+              : big_grouped_epi<TBM, TBN, WM, WN, true, false, float>(grp, g.epilogue, st);
+  return bk ? big_grouped_epi<TBM, TBN, WM, WN, true, true, bf16_t>(grp, g.epilogue, st)
+            : big_grouped_epi<TBM, TBN, WM, WN, true, false, bf16_t>(grp, g.epilogue, st);
+}
+
+int reduce_splits(const K3mGemm& g, hipStream_t st) {
   if (g.splitk > 1) {
     const long long total = (long long)g.m * g.n;
     const int blocks = (int)std::min<long long>((total + 255) / 256, 2048);
     hipLaunchKernelGGL(splitk_reduce_bf16_kernel, dim3(blocks), dim3(256), 0, st, g.ws, g.splitk, g.m, g.n,
                        static_cast<float*>(g.c), g.ldc, g.alpha, g.beta);
     K3M_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+bool vec_of(const K3mGemm& g) {
+  const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
+  const bool av = aligned16(g.a) && (g.lda % 8 == 0) && ((ak ? g.k : g.m) % 8 == 0);
+  const bool bv = aligned16(g.b) && (g.ldb % 8 == 0) && ((bk ? g.k : g.n) % 8 == 0);
+  return av && bv;
+}
+
+// K3M_BF16_BIG=0 keeps every bf16 GEMM on the 128x128 register-staged kernel (A/B switch)
+const bool kBig = [] {
+  const char* e = std::getenv("K3M_BF16_BIG");
+  return !(e && e[0] == '0');
+}();
+
+}  // namespace
+
+// Called by k3m_gemm (gemm.hip) for dtype == K3M_BF16; arguments already validated there.
+int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st) {
+  K3M_ARG(g.splitk <= 1 || g.c_dtype == K3M_F32);
+  const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
+  const bool vec = vec_of(g);
+  int rc;
+  const long long nb256 = nb_of(g, 256, 256), nb128 = nb_of(g, 256, 128);
+  if (kBig && big_ok(g, vec) && nb128 >= 160) {
+    rc = big_prefers_256(nb256) ? big_launch<256, 256, 2, 4>(g, st) : big_launch<256, 128, 4, 2>(g, st);
+  } else {
+    rc = g.c_dtype == K3M_F32 ? launch_ct<float>(g, ak, bk, vec, st) : launch_ct<bf16_t>(g, ak, bk, vec, st);
+  }
+  if (rc) return rc;
+  K3M_CHECK_LAUNCH();
+  return reduce_splits(g, st);
+}
+
+// Grouped bf16 problems (co-attention stages of the bf16 encoder): one large-tile grid when every
+// problem is eligible and shares the template (*handled = true), else nothing is launched.
+int k3m_gemm_bf16_grouped_impl(const K3mGemm* gs, int count, hipStream_t st, bool* handled) {
+  *handled = false;
+  if (!kBig || count <= 0 || count > k3m_b16::GROUP_MAX) return 0;
+  const K3mGemm& g0 = gs[0];
+  k3m_b16::GemmGroup grp = {};
+  int live = 0;
+  long long nb256 = 0, nb128 = 0;
+  for (int i = 0; i < count; ++i) {
+    const K3mGemm& g = gs[i];
+    if (g.dtype != K3M_BF16 || g.a_trans != g0.a_trans || g.b_trans != g0.b_trans || g.epilogue != g0.epilogue ||
+        g.c_dtype != g0.c_dtype || !big_ok(g, vec_of(g)) || (g.splitk > 1 && g.c_dtype != K3M_F32))
+      return 0;
+    if (g.m == 0 || g.n == 0) continue;
+    grp.g[live++] = g;
+    nb256 += nb_of(g, 256, 256);
+    nb128 += nb_of(g, 256, 128);
+  }
+  *handled = true;
+  if (live == 0) return 0;
+  const bool t256 = big_prefers_256(nb256);
+  int nb = 0;
+  for (int i = 0; i < live; ++i) {
+    grp.start[i] = nb;
+    nb += (int)nb_of(grp.g[i], 256, t256 ? 256 : 128);
+  }
+  grp.start[live] = nb;
+  grp.count = live;
+  const int rc = t256 ? big_grouped<256, 256, 2, 4>(grp, st) : big_grouped<256, 128, 4, 2>(grp, st);
+  if (rc) return rc;
+  K3M_CHECK_LAUNCH();
+  for (int i = 0; i < live; ++i) {
+    const int r = reduce_splits(grp.g[i], st);
+    if (r) return r;
   }
   return 0;
 }

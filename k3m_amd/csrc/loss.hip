@@ -166,6 +166,7 @@ extern "C" int k3m_compact_labels_ex(const int64_t* labels, int n, int64_t thres
 
 extern "C" int k3m_ce_fwd_bwd(float* logits, long long ld, const int64_t* labels, const float* row_scale, int rows,
                               int vocab, float* loss_rows, hipStream_t st) {
+  if (rows == 0) return 0;
   K3M_ARG(logits && labels && row_scale && loss_rows && rows >= 0 && vocab > 0);
   if (rows == 0) return 0;
   K3M_ARG(ld % 4 == 0);
@@ -176,6 +177,7 @@ extern "C" int k3m_ce_fwd_bwd(float* logits, long long ld, const int64_t* labels
 
 extern "C" int k3m_kl_fwd_bwd(float* logits, long long ld, const float* target, long long ldt, const int32_t* trow,
                               const float* row_scale, int rows, int ncls, float* loss_rows, hipStream_t st) {
+  if (rows == 0) return 0;
   K3M_ARG(logits && target && trow && row_scale && loss_rows && rows >= 0);
   if (rows == 0) return 0;
   hipLaunchKernelGGL(kl_kernel, dim3(rows), dim3(256), 0, st, logits, ld, target, ldt, trow, row_scale, ncls,

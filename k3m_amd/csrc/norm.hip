@@ -529,8 +529,8 @@ extern "C" int k3m_colsum(const void* x, long long ld, int rows, int cols, float
 }
 
 extern "C" int k3m_dgelu(const void* g, const void* pre, void* out, long long n, int dtype, hipStream_t st) {
-  K3M_ARG(g && pre && out);
   if (n == 0) return 0;
+  K3M_ARG(g && pre && out);
   DISPATCH_T(dtype, hipLaunchKernelGGL(dgelu_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, (const T*)g,
                                        (const T*)pre, (T*)out, n));
   K3M_CHECK_LAUNCH();
@@ -578,8 +578,8 @@ extern "C" int k3m_convert(const void* x, int xdtype, void* y, int ydtype, long 
 
 extern "C" int k3m_gather_rows(const void* src, long long lds, const int32_t* idx, int n, int cols, void* dst,
                                long long ldd, int dtype, hipStream_t st) {
+  if (n == 0) return 0;   // no labelled rows: nothing to move (buffers may be empty / NULL)
   K3M_ARG(src && idx && dst && n >= 0);
-  if (n == 0) return 0;
   DISPATCH_T(dtype, hipLaunchKernelGGL(gather_rows_kernel<T>, dim3(n), dim3(256), 0, st, (const T*)src, lds, idx, n,
                                        cols, (T*)dst, ldd));
   K3M_CHECK_LAUNCH();
@@ -588,8 +588,8 @@ extern "C" int k3m_gather_rows(const void* src, long long lds, const int32_t* id
 
 extern "C" int k3m_scatter_add_rows(const void* src, long long lds, const int32_t* idx, int n, int cols, void* dst,
                                     long long ldd, int dtype, hipStream_t st) {
+  if (n == 0) return 0;   // no labelled rows: nothing to move (buffers may be empty / NULL)
   K3M_ARG(src && idx && dst && n >= 0);
-  if (n == 0) return 0;
   DISPATCH_T(dtype, hipLaunchKernelGGL(scatter_add_rows_kernel<T>, dim3(n), dim3(256), 0, st, (const T*)src, lds, idx,
                                        n, cols, (T*)dst, ldd));
   K3M_CHECK_LAUNCH();

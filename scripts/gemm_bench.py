@@ -13,6 +13,7 @@ SHAPES = [
     ("fwd qkv", "nt", M, 2304, 768, L.EPI_BIAS),
     ("fwd out", "nt", M, 768, 768, L.EPI_BIAS),
     ("fwd ffn1 gelu", "nt", M, 3072, 768, L.EPI_BIAS_GELU),
+    ("fwd ffn1 plain", "nt", M, 3072, 768, L.EPI_NONE),
     ("fwd ffn2", "nt", M, 768, 3072, L.EPI_BIAS),
     ("dgrad qkv", "nn", M, 768, 2304, L.EPI_NONE),
     ("dgrad ffn2->dgelu", "nn", M, 3072, 768, L.EPI_DGELU),

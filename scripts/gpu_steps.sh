@@ -30,7 +30,9 @@ for s in "$@"; do
     spawn2) step spawn2 600 python bench.py --gpus 2 --steps 3 --warmup 1 --backend gloo --batch 16 ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
     benchq) step bench 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
-    profbf) export TMPDIR=/tmp; step profbf 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profbf -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --dtype bf16 ;;
+    profbf) export TMPDIR=/tmp; step profbf 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profbf -o run -- python bench.py --config 3 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    tbig) step tbig 600 python -u -m pytest tests/test_gpu_gemm_b16_big.py tests/test_gpu_gemm_bf16.py -v --timeout 300 --timeout-method thread ;;
+    ttrain) step ttrain 900 python -u -m pytest tests/test_gpu_trainer.py -v --timeout 300 --timeout-method thread ;;
     prof) export TMPDIR=/tmp; step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     gemm) step gemm 300 python scripts/gemm_bench.py all 10 both ;;
     gemmbf) step gemmbf 300 python scripts/gemm_bench.py all 10 bf16 ;;

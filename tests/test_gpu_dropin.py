@@ -1,0 +1,165 @@
+"""The drop-in boundary, driven the way train_concap_struc.py drives the reference:
+
+* imports through the ``vilbert_k3m`` package (train_concap_struc.py:25-26);
+* optimizer parameter groups built from ``model.named_parameters()`` (:352-367) and stepped by a
+  pytorch_transformers-AdamW optimizer (the oracle's restatement, pytorch_transformers being absent)
+  reading ``p.grad``;
+* the 10-tuple ``forward`` (:502-524), ``loss = mlm_t + img * w + mlm_pv + lpm`` (:531-533),
+  ``loss.backward()`` (:569), ``optimizer.step(); optimizer.zero_grad()`` (:573-574);
+* ``state_dict()`` with the reference's 999 keys (:691-705);
+* the loaders' iterator contract (dataset:413) feeding the model unchanged.
+Checked against the golden vectors recorded from the reference model (losses 1e-3, gradient norms
+5e-3, as tests/test_gpu_parity.py)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import HERE, load_case, case_config, case_batch, case_noise
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda")
+
+
+class RefAdamW(torch.optim.Optimizer):
+    """pytorch_transformers 1.1.0 AdamW semantics over param groups (oracle restatement)."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.0):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+
+    @torch.no_grad()
+    def step(self):
+        from oracle.k3m_oracle import adamw_step
+        for gr in self.param_groups:
+            for p in gr["params"]:
+                if p.grad is None:
+                    continue
+                st = self.state[p]
+                if not st:
+                    st["step"] = 0
+                    st["m"] = torch.zeros_like(p)
+                    st["v"] = torch.zeros_like(p)
+                st["step"] += 1
+                adamw_step(p.data, p.grad, st["m"], st["v"], st["step"], gr["lr"], gr["weight_decay"],
+                           gr["betas"][0], gr["betas"][1], gr["eps"])
+
+
+def _driver_forward(model, tb, dev, noise, ent, val):
+    return model(tb["input_ids"], tb["image_feat"], tb["image_loc"], tb["segment_ids"], tb["input_mask"],
+                 tb["image_mask"], tb["lm_label_ids"], tb["image_label"], tb["image_target"], tb["is_next"],
+                 output_all_attention_masks=False, input_ids_pv=tb["input_ids_pv"],
+                 token_type_ids_pv=tb["segment_ids_pv"], attention_mask_pv=tb["input_mask_pv"],
+                 masked_lm_labels_pv=tb["lm_label_ids_pv"], next_sentence_label_pv_v=tb["is_next_pv_v"],
+                 next_sentence_label_pv_t=tb["is_next_pv_t"], index_p=tb["index_p"], index_v=tb["index_v"],
+                 device=dev, gumbel_noise=noise, ent_neg=ent, val_neg=val)
+
+
+def test_driver_call_sequence_matches_golden(dev):
+    from vilbert_k3m.vilbert_k3m import BertForMultiModalPreTraining_tri_stru
+    from k3m_amd.weights import param_values
+    g = load_case("bs2_hard")
+    cfg = case_config(g)
+    model = BertForMultiModalPreTraining_tri_stru(cfg, device=dev)
+    vals = param_values(cfg, int(g["weight_seed"]))
+    missing = model.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()})
+    assert not missing
+    model.eval()
+    no_decay = ["bias", "LayerNorm.bias", "LayerNorm.weight"]
+    param_optimizer = list(model.named_parameters())
+    assert len(param_optimizer) == 998
+    groups = [{"params": [p for n, p in param_optimizer if not any(nd in n for nd in no_decay)], "weight_decay": 0.01},
+              {"params": [p for n, p in param_optimizer if any(nd in n for nd in no_decay)], "weight_decay": 0.0}]
+    opt = RefAdamW(groups, lr=1e-4, eps=1e-8, betas=(0.9, 0.98))
+    tb = {k: v.to(dev) for k, v in case_batch(g).items()}
+    noise = {k: v.to(dev) for k, v in case_noise(g).items()}
+    ent, val = torch.from_numpy(g["ent_neg"]), torch.from_numpy(g["val_neg"])
+    outs = _driver_forward(model, tb, dev, noise, ent, val)
+    assert len(outs) == 10
+    mlm_t, img, _, mlm_pv, _, _, nsp, c_init, c_final, lpm = outs
+    loss = mlm_t + img * 1.0 + mlm_pv + lpm
+    got = np.array([float(x) for x in (mlm_t, img, mlm_pv, lpm, nsp, loss)])
+    np.testing.assert_allclose(got, g["losses"], rtol=1e-3, atol=1e-4)
+    np.testing.assert_allclose(c_final.detach().cpu().numpy(), g["c_final"], rtol=1e-3, atol=1e-4)
+    loss.backward()
+    named = dict(model.named_parameters())
+    grads = {}
+    for n, ref in zip(list(g["grad_norm_names"]), g["grad_norms"]):
+        p = named[n]
+        gn = 0.0 if p.grad is None else float(p.grad.double().norm())
+        if np.isnan(ref):
+            assert gn == 0.0, n
+        else:
+            assert abs(gn - ref) <= 5e-3 * ref + 1e-6, (n, gn, ref)
+    for n in ("encoder.layer.0.attention.self.query.weight", "struc_w1.weight", "cls.predictions.bias",
+              "encoder.c_layer.2.biattention.key2.bias"):
+        grads[n] = named[n].grad.detach().cpu().clone()
+    before = {n: named[n].detach().cpu().clone() for n in grads}
+    opt.step()
+    from oracle.k3m_oracle import adamw_step
+    for n in grads:
+        p = before[n].clone()
+        adamw_step(p, grads[n], torch.zeros_like(p), torch.zeros_like(p), 1, 1e-4,
+                   0.0 if any(nd in n for nd in no_decay) else 0.01)
+        np.testing.assert_allclose(named[n].detach().cpu().numpy(), p.numpy(), rtol=1e-6, atol=1e-9, err_msg=n)
+    opt.zero_grad()
+    assert named["struc_w1.weight"].grad is None
+    # a second backward after zero_grad(set_to_none) starts from zero gradients (no stale sums)
+    outs = _driver_forward(model, tb, dev, noise, ent, val)
+    (outs[0] + outs[1] + outs[3] + outs[9]).backward()
+    g2 = named["struc_w1.weight"].grad
+    assert g2 is not None and torch.isfinite(g2).all()
+    sd = model.state_dict()
+    inv = json.load(open(os.path.join(HERE, "golden", "param_inventory.json")))   # the reference model's
+    assert [n for n, _ in model.named_parameters()] == [n for n, _ in inv["params"]]
+    assert len(sd) == 999 and sorted(sd) == sorted([n for n, _ in inv["params"]] + ["cls.predictions.decoder.weight"])
+    assert sd["cls.predictions.decoder.weight"].data_ptr() == sd["embeddings.word_embeddings.weight"].data_ptr()
+
+
+def test_loader_feeds_driver_loop(dev, tmp_path):
+    """ConceptCapLoaderTrain_struc with the driver's kwargs (incl. local_rank) on raw product rows:
+    the 19-item batches go straight into the model; the head buffers are sized without a sync."""
+    from vilbert_k3m.datasets import ConceptCapLoaderTrain_struc
+    from vilbert_k3m.vilbert_k3m import BertForMultiModalPreTraining_tri_stru
+    from k3m_amd.config import pretrain_config
+    from golden_util import CFG_PATH
+    from test_data import char_tokenizer
+    rows = []
+    for i in range(6):
+        pv = "#;#".join("p%d%d#:#v%d%d" % (i, j, j, i) for j in range(3 + i))
+        rows.append("%d\titem title %d with words\thttp://img/%d.jpg\t%s\tcat" % (1000 + i, i, i, pv))
+    (tmp_path / "train.tsv").write_text("\n".join(rows) + "\n", encoding="utf-8")
+    loader = ConceptCapLoaderTrain_struc(str(tmp_path), "train.tsv", char_tokenizer(), max_seq_len=36,
+                                         max_seq_len_pv=128, max_num_pv=20, max_region_len=36, batch_size=3,
+                                         visual_target=0, v_target_size=1601, num_workers=2, local_rank=0,
+                                         objective=2, cache=100, serializer=None, seed=1, synthetic_regions=3)
+    assert loader.num_dataset == 6 and len(loader) == 2
+    cfg = pretrain_config(CFG_PATH)
+    model = BertForMultiModalPreTraining_tri_stru(cfg, device=dev)
+    model.train()
+    n = 0
+    for step, batch in enumerate(loader):
+        index_p = torch.tensor(batch[-3]).cuda(device=dev, non_blocking=True)
+        index_v = torch.tensor(batch[-2]).cuda(device=dev, non_blocking=True)
+        batch = tuple(t.cuda(device=dev, non_blocking=True) for t in batch[:-3])
+        (input_ids, input_mask, segment_ids, lm_label_ids, is_next, input_ids_pv, input_mask_pv, segment_ids_pv,
+         lm_label_ids_pv, is_next_pv_v, is_next_pv_t, image_feat, image_loc, image_target, image_label,
+         image_mask) = batch
+        assert getattr(lm_label_ids, "_k3m_n_labels", None) is not None     # travels through .cuda()
+        outs = model(input_ids, image_feat, image_loc, segment_ids, input_mask, image_mask, lm_label_ids,
+                     image_label, image_target, is_next, output_all_attention_masks=False, input_ids_pv=input_ids_pv,
+                     token_type_ids_pv=segment_ids_pv, attention_mask_pv=input_mask_pv,
+                     masked_lm_labels_pv=lm_label_ids_pv, next_sentence_label_pv_v=is_next_pv_v,
+                     next_sentence_label_pv_t=is_next_pv_t, index_p=index_p, index_v=index_v, device=dev)
+        loss = outs[0] + outs[1] + outs[3] + outs[9]
+        loss.backward()
+        assert np.isfinite(float(loss))
+        n += 1
+    assert n == 2
