@@ -113,6 +113,49 @@ struct Shape {
   static constexpr int LDS = 2 * STAGE;                   // bf16 elements
 };
 
+// Accumulators of one wave's (WTM x WTN) output slab for the two MFMA shapes, and how a 32-row group
+// of them is staged into the epilogue's LDS image ([32][WS] fp32, row-major).
+template <int MF, int WTM, int WTN> struct Acc;
+template <int WTM, int WTN> struct Acc<16, WTM, WTN> {   // v_mfma_f32_16x16x32_bf16
+  static constexpr int FM = WTM / 16, FN = WTN / 16;
+  floatx4 v[FM][FN];
+  __device__ __forceinline__ void stage(int grp, float* wl, int ws, int lane) const {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wl[(16 * ii + 4 * (lane >> 4) + r) * ws + 16 * j + (lane & 15)] = v[2 * grp + ii][j][r];
+  }
+};
+template <int WTM, int WTN> struct Acc<32, WTM, WTN> {   // v_mfma_f32_32x32x16_bf16
+  static constexpr int FM = WTM / 32, FN = WTN / 32;
+  floatx16 v[FM][FN];
+  __device__ __forceinline__ void stage(int grp, float* wl, int ws, int lane) const {
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) wl[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * ws + 32 * j + (lane & 31)] = v[grp][j][r];
+  }
+};
+
+// 32x32x16 operand fragment: lane l gets X[mnb + (l & 31)][16 s + 8 (l >> 5) + e], e = 0..7 (s = 0..3)
+template <bool KC, int TILE>
+__device__ __forceinline__ bf16x8 frag32(const uint16_t* img, int mnb, int s, int lane) {
+  if constexpr (KC) {
+    return *reinterpret_cast<const bf16x8*>(img + kc_off(mnb + (lane & 31), 2 * s + (lane >> 5)));
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, h = lane >> 5;
+    const int ch = ((mnb + 16 * (g & 1)) >> 3) + (p >> 1);
+    const int r0 = 16 * s + 8 * h + q;
+    const short4v x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(img + mn_off<TILE>(r0, ch) + 4 * (p & 1)));
+    const short4v x1 =
+        __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(img + mn_off<TILE>(r0 + 4, ch) + 4 * (p & 1)));
+    const short8v v = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
 template <bool AK, bool BK_, int TBM, int TBN, int FM, int FN>
 __device__ __forceinline__ void read_frags(const uint16_t* stage, int wm, int wn, int s, int lane, bf16x8 (&a)[FM],
                                            bf16x8 (&b)[FN]) {
@@ -143,9 +186,10 @@ __device__ __forceinline__ void mfmas(floatx4 (&acc)[FM][FN], const bf16x8 (&a)[
 template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_>
 __device__ __forceinline__ void mainloop(const uint16_t* __restrict__ A, long long lda, const uint16_t* __restrict__ B,
                                          long long ldb, int M, int N, int m0, int n0, int kbeg, int kend,
-                                         uint16_t* smem, floatx4 (&acc)[TBM / WM / 16][TBN / WN / 16]) {
+                                         uint16_t* smem, Acc<16, TBM / WM, TBN / WN>& accs) {
   using S = Shape<TBM, TBN, WM, WN>;
   constexpr int FM = S::FM, FN = S::FN;
+  auto& acc = accs.v;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = (w / WN) * (TBM / WM), wn = (w % WN) * (TBN / WN);
 #pragma unroll
@@ -191,6 +235,85 @@ __device__ __forceinline__ void mainloop(const uint16_t* __restrict__ A, long lo
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();   // the epilogue reuses the stages
+}
+
+// The same pipeline with v_mfma_f32_32x32x16_bf16 and four 16-deep k-substeps per tile (fragment sets
+// Fa / Fb alternate): for the weight gradients, whose two MN-contiguous operands take two transposing
+// reads per fragment — 12 reads per substep keep every substep's reads inside the 15 outstanding LDS
+// operations a wave can count (the 24 of a 16x16x32 substep serialised the reads and the MFMAs).
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_>
+__device__ __forceinline__ void mainloop32(const uint16_t* __restrict__ A, long long lda,
+                                           const uint16_t* __restrict__ B, long long ldb, int M, int N, int m0,
+                                           int n0, int kbeg, int kend, uint16_t* smem,
+                                           Acc<32, TBM / WM, TBN / WN>& accs) {
+  using S = Shape<TBM, TBN, WM, WN>;
+  constexpr int FM = TBM / WM / 32, FN = TBN / WN / 32;
+  auto& acc = accs.v;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = (w / WN) * (TBM / WM), wn = (w % WN) * (TBN / WN);
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  Loader<AK, TBM, S::NT> la;
+  Loader<BK_, TBN, S::NT> lb;
+  la.init(A, lda, m0, kbeg, M);
+  lb.init(B, ldb, n0, kbeg, N);
+  const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
+  if (nk == 0) return;
+  la.issue(smem);
+  lb.issue(smem + TBM * BK);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (nk > 1) {
+    la.issue(smem + S::STAGE);
+    lb.issue(smem + S::STAGE + TBM * BK);
+  }
+  bf16x8 fa[FM], fb[FN], ga[FM], gb[FN];
+  auto rd = [&](const uint16_t* st, int sub, bf16x8(&a)[FM], bf16x8(&b)[FN]) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) a[i] = frag32<AK, TBM>(st, wm + 32 * i, sub, lane);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) b[j] = frag32<BK_, TBN>(st + TBM * BK, wn + 32 * j, sub, lane);
+  };
+  auto mm = [&](const bf16x8(&a)[FM], const bf16x8(&b)[FN]) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  };
+  rd(smem, 0, fa, fb);
+  for (int kt = 0; kt < nk; ++kt) {
+    uint16_t* cur = smem + (kt & 1) * S::STAGE;
+    uint16_t* nxt = smem + ((kt + 1) & 1) * S::STAGE;
+    rd(cur, 1, ga, gb);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    rd(cur, 2, fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(ga, gb);
+    __builtin_amdgcn_sched_barrier(0);
+    rd(cur, 3, ga, gb);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(fa, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 2 < nk) {
+      la.issue(cur);
+      lb.issue(cur + TBM * BK);
+    }
+    rd(nxt, 0, fa, fb);   // unconditional, as in mainloop
+    __builtin_amdgcn_sched_barrier(0);
+    mm(ga, gb);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
 }
 
 __device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
@@ -247,12 +370,11 @@ template <> struct Raw8<float> {
 // C, one for fp32 C (register budget) — a load issued right before its use exposed a full HBM latency
 // per row group and made the output-heavy epilogues latency-bound.
 // 16x16 accumulator layout: acc[i][j][r] = C[wm + 16 i + 4 (lane >> 4) + r][wn + 16 j + (lane & 15)].
-template <int TBM, int TBN, int WM, int WN, int EPI, typename CT>
-__device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint16_t* smem_u16,
-                                         floatx4 (&acc)[TBM / WM / 16][TBN / WN / 16], int slice) {
+template <int TBM, int TBN, int WM, int WN, int EPI, typename CT, typename AccT>
+__device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint16_t* smem_u16, const AccT& acc,
+                                         int slice) {
   using S = Shape<TBM, TBN, WM, WN>;
-  constexpr int FM = S::FM, FN = S::FN;
-  constexpr int WNC = TBN / WN, WS = WNC + 8, LPR = WNC / 8, RPP = 64 / LPR, NPS = 32 / RPP, NG = FM / 2;
+  constexpr int WNC = TBN / WN, WS = WNC + 8, LPR = WNC / 8, RPP = 64 / LPR, NPS = 32 / RPP, NG = TBM / WM / 32;
   static_assert(S::NT / 64 * 32 * WS * 4 <= S::LDS * 2, "epilogue staging exceeds the LDS stages");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = (w / WN) * (TBM / WM), wn = (w % WN) * WNC;
@@ -281,11 +403,11 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint1
   constexpr bool PRE = EPI == K3M_EPI_DGELU || CAN_OLD;
   constexpr int PD = (sizeof(CT) == 2 && NG >= 2) ? 2 : 1;   // groups in flight (register budget)
   Raw8<CT> pax[PRE && EPI == K3M_EPI_DGELU ? PD : 1][NPS], pold[PRE ? PD : 1][NPS];
-  auto row_of = [&](int i2, int ps) { return m0 + wm + 16 * i2 + ps * RPP + lr; };
+  auto row_of = [&](int grp, int ps) { return m0 + wm + 32 * grp + ps * RPP + lr; };
   auto prefetch = [&](int grp, int slot) {
 #pragma unroll
     for (int ps = 0; ps < NPS; ++ps) {
-      const int row = row_of(2 * grp, ps);
+      const int row = row_of(grp, ps);
       if (row < M && cvec && col + 8 <= N) {
         if constexpr (EPI == K3M_EPI_DGELU) pax[slot][ps].load(aux + (long long)row * g.ldaux + col);
         if constexpr (CAN_OLD) {
@@ -300,19 +422,13 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint1
   }
 #pragma unroll
   for (int grp = 0; grp < NG; ++grp) {
-    const int i2 = 2 * grp;
     const int slot = grp % PD;
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) wl[(16 * ii + 4 * (lane >> 4) + r) * WS + 16 * j + (lane & 15)] = acc[i2 + ii][j][r];
+    acc.stage(grp, wl, WS, lane);
     __syncthreads();
 #pragma unroll
     for (int ps = 0; ps < NPS; ++ps) {
       const int rr = ps * RPP + lr;
-      const int row = row_of(i2, ps);
+      const int row = row_of(grp, ps);
       const floatx4 v0 = *reinterpret_cast<const floatx4*>(wl + rr * WS + lc);
       const floatx4 v1 = *reinterpret_cast<const floatx4*>(wl + rr * WS + lc + 4);
       if (row >= M || col >= N) continue;
@@ -403,6 +519,21 @@ struct GemmGroup {
   int count;
 };
 
+// one output tile: MN x MN (weight gradients) on 32x32x16 MFMAs, everything else on 16x16x32
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT>
+__device__ __forceinline__ void run_tile(const K3mGemm& g, int m0, int n0, int kbeg, int kend, int slice,
+                                         uint16_t* smem) {
+  constexpr int MF = (!AK && !BK_) ? 32 : 16;
+  Acc<MF, TBM / WM, TBN / WN> acc;
+  if constexpr (MF == 32)
+    mainloop32<TBM, TBN, WM, WN, AK, BK_>(static_cast<const uint16_t*>(g.a), g.lda, static_cast<const uint16_t*>(g.b),
+                                          g.ldb, g.m, g.n, m0, n0, kbeg, kend, smem, acc);
+  else
+    mainloop<TBM, TBN, WM, WN, AK, BK_>(static_cast<const uint16_t*>(g.a), g.lda, static_cast<const uint16_t*>(g.b),
+                                        g.ldb, g.m, g.n, m0, n0, kbeg, kend, smem, acc);
+  epilogue<TBM, TBN, WM, WN, EPI, CT>(g, m0, n0, smem, acc, slice);
+}
+
 template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(K3mGemm g) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[Shape<TBM, TBN, WM, WN>::LDS];
@@ -412,10 +543,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(K3mGemm g) {
   int m0, n0, slice, kbeg, kend;
   coords(id, g.m, g.n, TBM, TBN, m0, n0, slice);
   k_range(g, slice, kbeg, kend);
-  floatx4 acc[TBM / WM / 16][TBN / WN / 16];
-  mainloop<TBM, TBN, WM, WN, AK, BK_>(static_cast<const uint16_t*>(g.a), g.lda, static_cast<const uint16_t*>(g.b),
-                                      g.ldb, g.m, g.n, m0, n0, kbeg, kend, smem, acc);
-  epilogue<TBM, TBN, WM, WN, EPI, CT>(g, m0, n0, smem, acc, slice);
+  run_tile<TBM, TBN, WM, WN, AK, BK_, EPI, CT>(g, m0, n0, kbeg, kend, slice, smem);
 }
 
 // several independent problems sharing the template in one grid: blocks [start[p], start[p+1]) are
@@ -430,10 +558,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_grouped_kernel(GemmGroup
   int m0, n0, slice, kbeg, kend;
   coords(id - grp.start[p], g.m, g.n, TBM, TBN, m0, n0, slice);
   k_range(g, slice, kbeg, kend);
-  floatx4 acc[TBM / WM / 16][TBN / WN / 16];
-  mainloop<TBM, TBN, WM, WN, AK, BK_>(static_cast<const uint16_t*>(g.a), g.lda, static_cast<const uint16_t*>(g.b),
-                                      g.ldb, g.m, g.n, m0, n0, kbeg, kend, smem, acc);
-  epilogue<TBM, TBN, WM, WN, EPI, CT>(g, m0, n0, smem, acc, slice);
+  run_tile<TBM, TBN, WM, WN, AK, BK_, EPI, CT>(g, m0, n0, kbeg, kend, slice, smem);
 }
 
 }  // namespace k3m_b16

@@ -441,9 +441,8 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 bool big_ok(const K3mGemm& g, bool vec) {
   if (!vec || g.k % k3m_b16::BK != 0 || g.k == 0) return false;
   const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
-  // weight gradients (both operands MN-contiguous: two transposing reads per fragment on both sides)
-  // measured 2x slower on this kernel than on the 128x128 register-staged one: they stay there
-  if (!ak) return false;
+  if (!ak && bk) return false;
+  if (!ak && !(g.epilogue == K3M_EPI_NONE && g.c_dtype == K3M_F32)) return false;   // weight gradients
   if (g.splitk > 1 && ((g.k + g.splitk - 1) / g.splitk) < k3m_b16::BK) return false;
   return true;
 }

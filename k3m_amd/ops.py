@@ -189,6 +189,17 @@ def _splitk(m, n, k, dtype=torch.float32):
             if cost < best_cost - 1e-9:
                 best, best_cost = s, cost
         return best
+    if dtype == torch.bfloat16 and k % 64 == 0 and m % 8 == 0 and n % 8 == 0:
+        # the large-tile bf16 kernel (gemm_b16_tile.h): 256x256 blocks, one per CU; >= 16 k-tiles per split
+        tiles = ((m + 255) // 256) * ((n + 255) // 256)
+        if tiles >= 192 or k < 2048:
+            return 1
+        best, best_cost = 1, float("inf")
+        for s in range(1, min(32, k // 1024) + 1):
+            cost = ((tiles * s + 255) // 256) / s * (1.0 + 0.02 * s)
+            if cost < best_cost - 1e-9:
+                best, best_cost = s, cost
+        return best
     tiles = ((m + 127) // 128) * ((n + 127) // 128)
     if tiles >= 384 or k < 1024:
         return 1
