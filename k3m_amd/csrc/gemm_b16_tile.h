@@ -519,11 +519,10 @@ struct GemmGroup {
   int count;
 };
 
-// one output tile: MN x MN (weight gradients) on 32x32x16 MFMAs, everything else on 16x16x32
-template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT>
+// one output tile on MF x MF x (512 / MF) MFMAs (MF = 16 or 32)
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF>
 __device__ __forceinline__ void run_tile(const K3mGemm& g, int m0, int n0, int kbeg, int kend, int slice,
                                          uint16_t* smem) {
-  constexpr int MF = (!AK && !BK_) ? 32 : 16;
   Acc<MF, TBM / WM, TBN / WN> acc;
   if constexpr (MF == 32)
     mainloop32<TBM, TBN, WM, WN, AK, BK_>(static_cast<const uint16_t*>(g.a), g.lda, static_cast<const uint16_t*>(g.b),
@@ -534,7 +533,7 @@ __device__ __forceinline__ void run_tile(const K3mGemm& g, int m0, int n0, int k
   epilogue<TBM, TBN, WM, WN, EPI, CT>(g, m0, n0, smem, acc, slice);
 }
 
-template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT>
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(K3mGemm g) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[Shape<TBM, TBN, WM, WN>::LDS];
   const int tm = (g.m + TBM - 1) / TBM, tn = (g.n + TBN - 1) / TBN;
@@ -543,12 +542,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(K3mGemm g) {
   int m0, n0, slice, kbeg, kend;
   coords(id, g.m, g.n, TBM, TBN, m0, n0, slice);
   k_range(g, slice, kbeg, kend);
-  run_tile<TBM, TBN, WM, WN, AK, BK_, EPI, CT>(g, m0, n0, kbeg, kend, slice, smem);
+  run_tile<TBM, TBN, WM, WN, AK, BK_, EPI, CT, MF>(g, m0, n0, kbeg, kend, slice, smem);
 }
 
 // several independent problems sharing the template in one grid: blocks [start[p], start[p+1]) are
 // problem p (split-major: slice, tile)
-template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT>
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_grouped_kernel(GemmGroup grp) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[Shape<TBM, TBN, WM, WN>::LDS];
   const int id = xcd_remap(blockIdx.x, grp.start[grp.count]);
@@ -558,7 +557,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_grouped_kernel(GemmGroup
   int m0, n0, slice, kbeg, kend;
   coords(id - grp.start[p], g.m, g.n, TBM, TBN, m0, n0, slice);
   k_range(g, slice, kbeg, kend);
-  run_tile<TBM, TBN, WM, WN, AK, BK_, EPI, CT>(g, m0, n0, kbeg, kend, slice, smem);
+  run_tile<TBM, TBN, WM, WN, AK, BK_, EPI, CT, MF>(g, m0, n0, kbeg, kend, slice, smem);
 }
 
 }  // namespace k3m_b16

@@ -451,13 +451,22 @@ long long nb_of(const K3mGemm& g, int bm, int bn) {
   return (long long)((g.m + bm - 1) / bm) * ((g.n + bn - 1) / bn) * (g.splitk > 1 ? g.splitk : 1);
 }
 
-template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, typename CT>
-int big_launch_epi(const K3mGemm& g, hipStream_t st) {
+// MFMA shape per operand layout: 16x16x32 when B is K-contiguous (forward), 32x32x16 when it is
+// MN-contiguous (input and weight gradients: their transposing fragment reads fit the LDS counter
+// per 16-deep substep); K3M_B16_MF=16 / 32 forces one shape everywhere (A/B).
+const int kMF = [] {
+  const char* e = std::getenv("K3M_B16_MF");
+  return e ? std::atoi(e) : 0;
+}();
+inline bool use_mf32(bool bk) { return kMF == 32 || (kMF != 16 && !bk); }
+
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, typename CT, int MF>
+int big_launch_epi_mf(const K3mGemm& g, hipStream_t st) {
   const dim3 grid((unsigned)nb_of(g, TBM, TBN));
   switch (g.epilogue) {
 #define K3M_GEMM_CASE(E)                                                                                     \
     case E:                                                                                                  \
-      hipLaunchKernelGGL((k3m_b16::gemm_kernel<TBM, TBN, WM, WN, AK, BK_, E, CT>), grid, dim3(64 * WM * WN), 0, st, g); \
+      hipLaunchKernelGGL((k3m_b16::gemm_kernel<TBM, TBN, WM, WN, AK, BK_, E, CT, MF>), grid, dim3(64 * WM * WN), 0, st, g); \
       break;
     K3M_GEMM_CASE(K3M_EPI_NONE)
     K3M_GEMM_CASE(K3M_EPI_BIAS)
@@ -470,12 +479,18 @@ int big_launch_epi(const K3mGemm& g, hipStream_t st) {
   return 0;
 }
 
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, typename CT>
+int big_launch_epi(const K3mGemm& g, hipStream_t st) {
+  return use_mf32(BK_) ? big_launch_epi_mf<TBM, TBN, WM, WN, AK, BK_, CT, 32>(g, st)
+                       : big_launch_epi_mf<TBM, TBN, WM, WN, AK, BK_, CT, 16>(g, st);
+}
+
 template <int TBM, int TBN, int WM, int WN>
 int big_launch(const K3mGemm& g, hipStream_t st) {
   const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
   if (!ak) {
     if (g.epilogue != K3M_EPI_NONE) return K3M_EINVAL;
-    hipLaunchKernelGGL((k3m_b16::gemm_kernel<TBM, TBN, WM, WN, false, false, K3M_EPI_NONE, float>),
+    hipLaunchKernelGGL((k3m_b16::gemm_kernel<TBM, TBN, WM, WN, false, false, K3M_EPI_NONE, float, 32>),
                        dim3((unsigned)nb_of(g, TBM, TBN)), dim3(64 * WM * WN), 0, st, g);
     return 0;
   }
@@ -489,14 +504,14 @@ int big_launch(const K3mGemm& g, hipStream_t st) {
 // tile policy: 256x256 when it still gives >= ~3/4 of a wave of blocks, else 256x128
 bool big_prefers_256(long long nb256) { return nb256 >= 192; }
 
-template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, typename CT>
-int big_grouped_epi(const k3m_b16::GemmGroup& grp, int epi, hipStream_t st) {
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, typename CT, int MF>
+int big_grouped_epi_mf(const k3m_b16::GemmGroup& grp, int epi, hipStream_t st) {
   const dim3 grid(grp.start[grp.count]);
   switch (epi) {
 #define K3M_GROUP_CASE(E)                                                                                      \
     case E:                                                                                                    \
-      hipLaunchKernelGGL((k3m_b16::gemm_grouped_kernel<TBM, TBN, WM, WN, AK, BK_, E, CT>), grid, dim3(64 * WM * WN), 0, \
-                         st, grp);                                                                             \
+      hipLaunchKernelGGL((k3m_b16::gemm_grouped_kernel<TBM, TBN, WM, WN, AK, BK_, E, CT, MF>), grid, dim3(64 * WM * WN), \
+                         0, st, grp);                                                                          \
       break;
     K3M_GROUP_CASE(K3M_EPI_NONE)
     K3M_GROUP_CASE(K3M_EPI_BIAS)
@@ -509,13 +524,19 @@ int big_grouped_epi(const k3m_b16::GemmGroup& grp, int epi, hipStream_t st) {
   return 0;
 }
 
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, typename CT>
+int big_grouped_epi(const k3m_b16::GemmGroup& grp, int epi, hipStream_t st) {
+  return use_mf32(BK_) ? big_grouped_epi_mf<TBM, TBN, WM, WN, AK, BK_, CT, 32>(grp, epi, st)
+                       : big_grouped_epi_mf<TBM, TBN, WM, WN, AK, BK_, CT, 16>(grp, epi, st);
+}
+
 template <int TBM, int TBN, int WM, int WN>
 int big_grouped(const k3m_b16::GemmGroup& grp, hipStream_t st) {
   const K3mGemm& g = grp.g[0];
   const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
   if (!ak) {
     if (g.epilogue != K3M_EPI_NONE) return K3M_EINVAL;
-    hipLaunchKernelGGL((k3m_b16::gemm_grouped_kernel<TBM, TBN, WM, WN, false, false, K3M_EPI_NONE, float>),
+    hipLaunchKernelGGL((k3m_b16::gemm_grouped_kernel<TBM, TBN, WM, WN, false, false, K3M_EPI_NONE, float, 32>),
                        dim3(grp.start[grp.count]), dim3(64 * WM * WN), 0, st, grp);
     return 0;
   }

@@ -49,7 +49,7 @@ def run(name, kind, m, n, k, epi, reps=10, dtype=torch.float32):
     bias = torch.zeros(n, device=dev)
     aux = torch.randn(m, n, device=dev, dtype=cdt) if epi in (L.EPI_BIAS_GELU, L.EPI_DGELU) else None
     beta = 1.0 if kind == "tn" else 0.0
-    s = ops._splitk(m, n, k) if kind == "tn" else 1
+    s = ops._splitk(m, n, k, dtype) if kind == "tn" else 1
     ws = torch.empty(s * m * n, device=dev) if s > 1 else None
 
     def go():

@@ -1,0 +1,45 @@
+"""From a rocprofv3 kernel trace of bench.py: GPU kernel time inside the timed steps vs the wall time
+of those steps (is the step GPU-bound or launch-bound?).  Usage: step_time_split.py trace.csv steps"""
+import csv
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+steps = int(sys.argv[2])
+ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+# the timed region: the last `steps` occurrences of the step's first kernel (the embedding forward)
+starts = [s for s, e, n in ev if "embed_fwd" in n]
+first_per_step = starts[::2]          # two embed_fwd launches per step (text, PV)
+t0 = first_per_step[-steps]
+t1 = ev[-1][1]
+busy = 0
+cur_s, cur_e = None, None
+n = 0
+for s, e, name in ev:
+    if s < t0:
+        continue
+    n += 1
+    if cur_e is None or s > cur_e:
+        if cur_e is not None:
+            busy += cur_e - cur_s
+        cur_s, cur_e = s, e
+    else:
+        cur_e = max(cur_e, e)
+busy += cur_e - cur_s
+wall = t1 - t0
+print("timed steps %d: wall %.2f ms/step, GPU busy %.2f ms/step (%.1f%%), %d kernels/step" % (
+    steps, wall / 1e6 / steps, busy / 1e6 / steps, 100.0 * busy / wall, n // steps))
+
+# per-kernel-family time inside the timed steps
+import collections
+import re
+fam = collections.defaultdict(lambda: [0, 0])
+for s, e, name in ev:
+    if s < t0:
+        continue
+    key = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    key = re.sub(r"\(.*", "", key)[:90]
+    fam[key][0] += e - s
+    fam[key][1] += 1
+tot = sum(v[0] for v in fam.values())
+for k, (t, c) in sorted(fam.items(), key=lambda kv: -kv[1][0])[:int(sys.argv[3]) if len(sys.argv) > 3 else 30]:
+    print("%-90s %5d/step %8.3f ms/step %5.1f%%" % (k, c // steps, t / 1e6 / steps, 100.0 * t / tot))
