@@ -33,6 +33,7 @@ for s in "$@"; do
     profbf) export TMPDIR=/tmp; step profbf 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profbf -o run -- python bench.py --config 3 --steps 3 --warmup 1 --no-cpu-baseline ;;
     profbf10) export TMPDIR=/tmp; step profbf10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profbf10 -o run -- python bench.py --config 3 --steps 10 --warmup 2 --no-cpu-baseline ;;
     tbig) step tbig 600 python -u -m pytest tests/test_gpu_gemm_b16_big.py tests/test_gpu_gemm_bf16.py -v --timeout 300 --timeout-method thread ;;
+    ddpeng) step ddpeng 400 python -u -m pytest tests/test_gpu_ddp_engine.py -v -s --timeout 300 --timeout-method thread ;;
     ttrain) step ttrain 900 python -u -m pytest tests/test_gpu_trainer.py -v --timeout 300 --timeout-method thread ;;
     prof) export TMPDIR=/tmp; step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     gemm) step gemm 300 python scripts/gemm_bench.py all 10 both ;;
