@@ -200,8 +200,9 @@ class FFN(object):
 
 def _flash(q, hd, lq, lk):
     # bf16 encoder: the LSE-saving bf16 kernels (attention_bf16.hip, L <= 128); fp32 and longer
-    # sequences: the exact-fp32 kernels (attention.hip, attention_long.hip)
-    return q.dtype == torch.bfloat16 and hd in (64, 96, 128) and max(lq, lk) <= ops.SHORT_MAXL
+    # sequences (or a 128 x 128 head-dim-128 co-attention whose backward images exceed the LDS): the
+    # exact-fp32 kernels (attention.hip, attention_long.hip), which also read/write bf16
+    return q.dtype == torch.bfloat16 and ops.flash_fits(lq, lk, hd)
 
 
 def _attn_fwd(q, k, v, mask, nseq, lq, lk, nh, p, rng, out=None):

@@ -273,16 +273,43 @@ def embed_bwd(ids, tt, ds, dword, dpos, dtyp):
 
 # ------------------------------------------------------------------ attention
 SHORT_MAXL = 128   # attention.hip keeps a whole head in LDS up to this length; attention_long.hip beyond
+LDS_MAX = 160 * 1024
+
+
+def _r32(n):
+    return (n + 31) & ~31
+
+
+def _short_fits(lq, lk, hd, bwd):
+    """attention.hip's whole-head LDS images (fwd_lds / bwd_lds there) fit one CU's 160 KB; the
+    largest shapes (e.g. 128 x 128 keys at head dim 128: seq_len 128 text <-> 128 PV co-attention,
+    BASELINE configs[3]) go to the chunked attention_long.hip kernels instead."""
+    if max(lq, lk) > SHORT_MAXL:
+        return False
+    LQ, LK = _r32(lq), _r32(lk)
+    if not bwd:
+        return 4 * (LQ * hd + LK * hd + LQ * LK) <= LDS_MAX
+    r2n = max(LK * hd, LQ * LK)
+    return 4 * (LQ * hd + r2n + LQ * LK + (0 if LK * hd + LQ <= r2n else LQ)) <= LDS_MAX
+
+
+def flash_fits(lq, lk, hd):
+    """attention_bf16.hip's LDS images (its fwd_lds / bwd_lds; the backward is the larger) fit 160 KB."""
+    if max(lq, lk) > SHORT_MAXL or hd not in (64, 96, 128):
+        return False
+    LQ, LK, h = _r32(lq), _r32(lk), 128 if hd == 96 else hd
+    PW = 128 if LK == 96 else LK
+    return 2 * (2 * LQ * h + 2 * LK * h + 2 * LQ * PW) + 4 * (LK + 2 * LQ) <= LDS_MAX
 
 
 def attn_fwd(q, k, v, kmask, ctx, probs, nseq, lq, lk, nh, hd, scale, p_drop, seed, off):
-    name = "k3m_attn_fwd" if max(lq, lk) <= SHORT_MAXL else "k3m_attn_long_fwd"
+    name = "k3m_attn_fwd" if _short_fits(lq, lk, hd, False) else "k3m_attn_long_fwd"
     call(name, ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v), ptr(kmask), ptr(ctx), _ld(ctx), ptr(probs),
          nseq, lq, lk, nh, hd, scale, p_drop, seed, off, dt(ctx), stream())
 
 
 def attn_bwd(dctx, o, q, k, v, probs, dq, dk, dv, nseq, lq, lk, nh, hd, scale, p_drop, seed, off):
-    if max(lq, lk) <= SHORT_MAXL:
+    if _short_fits(lq, lk, hd, True):
         call("k3m_attn_bwd", ptr(dctx), _ld(dctx), ptr(o), _ld(o), ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v),
              ptr(probs), ptr(dq), ptr(dk), ptr(dv), _ld(dq), _ld(dk), _ld(dv), nseq, lq, lk, nh, hd, scale, p_drop,
              seed, off, dt(dctx), stream())

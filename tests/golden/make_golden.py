@@ -93,14 +93,14 @@ def synth_regions(rng, nbox=36, feat=2048, cls=1601):
     return h, w, nbox, boxes, f, p
 
 
-def build_batch(pre, rows, seed):
+def build_batch(pre, rows, seed, nbox=36):
     random.seed(seed)
     np.random.seed(seed)
     rng = np.random.default_rng(seed)
     samples = []
     for r in rows:
         item_id, title, _url, pv, cate = r
-        h, w, nb, boxes, f, p = synth_regions(rng)
+        h, w, nb, boxes, f, p = synth_regions(rng, nbox=nbox)
         samples.append(pre((item_id, title, pv, cate, h, w, nb, boxes, f, p)))
     cols = list(zip(*samples))
     (item_id, input_ids, input_mask, segment_ids, lm_label_ids, is_next, input_ids_pv, input_mask_pv,
@@ -143,8 +143,22 @@ SLICE_GRADS = ["encoder.layer.0.attention.self.query.weight", "encoder.layer.6.i
                "embeddings.word_embeddings.weight", "cls.predictions.bias"]
 
 
+def many_triples(rows, n):
+    """A knowledge-heavy PV field (configs[4]: 50 triples per product): n short key:value triples
+    (2-character keys and values) drawn from the PV fields of the raw rows, in the raw '#:#' / '#;#' format."""
+    out = []
+    for r in rows:
+        for kv in r[3].split("#;#"):
+            if "#:#" in kv:
+                k, v = kv.split("#:#", 1)
+                out.append("%s#:#%s" % (k[:2], v[:2]))
+                if len(out) == n:
+                    return "#;#".join(out)
+    raise ValueError("not enough triples")
+
+
 def run_case(name, row_ids, data_seed, weight_seed, noise_seed, neg_seed, mode=1, T=36, P=128, NPV=20,
-             drop_pv_of=()):
+             drop_pv_of=(), R=36, triples=None, long_title=0):
     import vilbert_k3m.vilbert_k3m as K
     from vilbert_k3m.datasets.concept_cap_dataset_struc import BertPreprocessBatch
     from k3m_amd.config import pretrain_config
@@ -155,8 +169,18 @@ def run_case(name, row_ids, data_seed, weight_seed, noise_seed, neg_seed, mode=1
     rows = [rows[i] for i in row_ids]
     for i in drop_pv_of:          # an item with no property-value triple (exercises the zero-triple quirk)
         rows[i] = rows[i][:3] + ["no-properties-here"] + rows[i][4:]
-    pre = BertPreprocessBatch(CharTokenizer(), max_seq_len=T, max_seq_len_pv=P, max_num_pv=NPV, max_region_len=36)
-    batch = build_batch(pre, rows, data_seed)
+    if long_title:                # fill a long text sequence: titles of the following rows appended
+        every = [l.rstrip("\n").split("\t") for l in open(os.path.join(REF, "data/raw_multidata_of_product_preatrain.small_train"),
+                                                             encoding="utf-8")]
+        for i, rid in enumerate(row_ids):
+            rows[i] = [rows[i][0], "".join(every[rid + j][1] for j in range(long_title))] + rows[i][2:]
+    if triples:
+        every = [l.rstrip("\n").split("\t") for l in open(os.path.join(REF, "data/raw_multidata_of_product_preatrain.small_train"),
+                                                             encoding="utf-8")]
+        for i in range(len(rows)):
+            rows[i] = rows[i][:3] + [many_triples(every[7 * i:], triples)] + rows[i][4:]
+    pre = BertPreprocessBatch(CharTokenizer(), max_seq_len=T, max_seq_len_pv=P, max_num_pv=NPV, max_region_len=R)
+    batch = build_batch(pre, rows, data_seed, nbox=R)
 
     cfg_path = os.path.join(REPO, "configs/bert_base_6layer_6conect.json")
     cfg = pretrain_config(cfg_path, if_pre_sampling=mode)
@@ -173,13 +197,18 @@ def run_case(name, row_ids, data_seed, weight_seed, noise_seed, neg_seed, mode=1
     model.eval()
 
     B = batch["input_ids"].shape[0]
-    shapes = [("v", (B, 37, 3, 1024)), ("t", (B, T, 3, 768)), ("pv", (B, P, 3, 768))]
+    shapes = [("v", (B, R + 1, 3, 1024)), ("t", (B, T, 3, 768)), ("pv", (B, P, 3, 768))]
     noise = {k: torch.from_numpy(v) for k, v in gumbel_noise(noise_seed, shapes).items()}
     order = {}
 
     def fake_gumbel(logits, tau=1.0, hard=False, eps=1e-10, dim=-1):
         L = logits.shape[1]
-        key = "v" if logits.shape[-1] == 1024 else ("t" if L == T else "pv")
+        if logits.shape[-1] == 1024:
+            key = "v"
+        elif T != P:
+            key = "t" if L == T else "pv"
+        else:                       # T == P: the reference pre-samples t before pv (vilbert_k3m.py:2382-2387)
+            key = "pv" if "t" in order else "t"
         order.setdefault(key, len(order))
         g = noise[key]
         y = ((logits + g) / tau).softmax(dim)
@@ -254,10 +283,22 @@ def run_case(name, row_ids, data_seed, weight_seed, noise_seed, neg_seed, mode=1
     print(name, "losses", res["losses"], "->", path, os.path.getsize(path) // 1024, "KiB")
 
 
+CASES = {
+    "bs2_hard": dict(row_ids=[0, 1], data_seed=7, weight_seed=1234, noise_seed=11, neg_seed=42, mode=1),
+    "bs3_zero_triple": dict(row_ids=[4, 2, 9], data_seed=8, weight_seed=99, noise_seed=12, neg_seed=43, mode=1,
+                            drop_pv_of=(0,)),
+    "bs2_mean": dict(row_ids=[3, 5], data_seed=9, weight_seed=7, noise_seed=13, neg_seed=44, mode=0),
+    # configs[3]: seq_len 128, 100 region boxes
+    "cfg4_bs2": dict(row_ids=[6, 11], data_seed=10, weight_seed=4, noise_seed=14, neg_seed=45, mode=1, T=128, R=100,
+                     long_title=4),
+    # configs[4]: knowledge-heavy, 50 PV triples per product in a 320-token PV sequence
+    "cfg5_bs2": dict(row_ids=[8, 12], data_seed=11, weight_seed=5, noise_seed=15, neg_seed=46, mode=1, P=320, NPV=50,
+                     triples=50),
+}
+
+
 if __name__ == "__main__":
     _stub_imports()
     torch.set_num_threads(8)
-    run_case("bs2_hard", [0, 1], data_seed=7, weight_seed=1234, noise_seed=11, neg_seed=42, mode=1)
-    run_case("bs3_zero_triple", [4, 2, 9], data_seed=8, weight_seed=99, noise_seed=12, neg_seed=43, mode=1,
-             drop_pv_of=(0,))
-    run_case("bs2_mean", [3, 5], data_seed=9, weight_seed=7, noise_seed=13, neg_seed=44, mode=0)
+    for name in (sys.argv[1:] or list(CASES)):
+        run_case(name, **CASES[name])

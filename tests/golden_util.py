@@ -6,7 +6,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-CASES = ["bs2_hard", "bs3_zero_triple", "bs2_mean"]
+CASES = ["bs2_hard", "bs3_zero_triple", "bs2_mean", "cfg4_bs2", "cfg5_bs2"]
 CFG_PATH = os.path.join(REPO, "configs", "bert_base_6layer_6conect.json")
 
 
