@@ -94,6 +94,13 @@ int k3m_ln_fwd(const void* x, const void* res, const float* gamma, const float* 
 int k3m_ln_bwd(const void* dy, const void* xhat, const float* rstd, const float* gamma, void* dres, void* dx,
                float* dgamma, float* dbeta, float* dxsum, int rows, int cols, float p_in, float p_out, uint64_t seed,
                uint64_t off_in, uint64_t off_out, int accumulate_res, float* ws, int dtype, hipStream_t stream);
+/* k3m_ln_bwd without the reduction: dres/dx written, the dgamma / dbeta / (want_sum) sum(dx)
+ * column partials left as 3 arrays of k3m_ln_bwd_nslab(rows) slabs (array a at ws + a*nslab*cols)
+ * for k3m_slab_reduce_batch. */
+int k3m_ln_bwd_nslab(int rows);
+int k3m_ln_bwd_slabs(const void* dy, const void* xhat, const float* rstd, const float* gamma, void* dres, void* dx,
+                     int rows, int cols, float p_in, float p_out, uint64_t seed, uint64_t off_in, uint64_t off_out,
+                     int accumulate_res, int want_sum, float* ws, int dtype, hipStream_t stream);
 
 /* BertEmbeddings (vilbert_k3m.py:361-382): word + position + token-type -> LN -> dropout.
  * The row is written to y0 and, when non-NULL, to y1 and y2 (the same embedding output feeds two

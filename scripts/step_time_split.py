@@ -43,3 +43,19 @@ for s, e, name in ev:
 tot = sum(v[0] for v in fam.values())
 for k, (t, c) in sorted(fam.items(), key=lambda kv: -kv[1][0])[:int(sys.argv[3]) if len(sys.argv) > 3 else 30]:
     print("%-90s %5d/step %8.3f ms/step %5.1f%%" % (k, c // steps, t / 1e6 / steps, 100.0 * t / tot))
+
+# the largest (kernel, grid) classes: which launches of a family cost most
+if len(sys.argv) > 4:
+    cls = collections.defaultdict(lambda: [0, 0])
+    for r in rows:
+        s = int(r["Start_Timestamp"])
+        if s < t0:
+            continue
+        key = re.sub(r"\(.*", "", r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", ""))[:70]
+        g = "%sx%sx%s/%s lds%s" % (r.get("Grid_Size_X", "?"), r.get("Grid_Size_Y", "?"), r.get("Grid_Size_Z", "?"),
+                                  r.get("Workgroup_Size_X", "?"), r.get("LDS_Block_Size", r.get("Lds_Size", "?")))
+        cls[(key, g)][0] += int(r["End_Timestamp"]) - s
+        cls[(key, g)][1] += 1
+    print("\ntop (kernel, grid) classes")
+    for (k, g), (t, c) in sorted(cls.items(), key=lambda kv: -kv[1][0])[:int(sys.argv[4])]:
+        print("%-70s %-28s %4d/step %7.3f ms/step  %7.1f us avg" % (k, g, c // steps, t / 1e6 / steps, t / 1e3 / c))
