@@ -77,6 +77,16 @@ int k3m_gemm_grouped(const K3mGemm* gs, int count, hipStream_t stream);
  * ws: >= (256 + 16)*cols floats. */
 int k3m_colsum(const void* x, long long ld, int rows, int cols, float* out, int accumulate, float* ws,
                int dtype, hipStream_t stream);
+/* k3m_colsum without the reduction: nslab (k3m_colsum_nslab) fp32 slabs of column partials at ws
+ * ([nslab][cols]) for k3m_slab_reduce_batch. */
+int k3m_colsum_nslab(int rows, int* nslab);
+int k3m_colsum_slabs(const void* x, long long ld, int rows, int cols, float* ws, int dtype, hipStream_t stream);
+/* Deterministic column-slab reduction of njobs independent jobs (host arrays of njobs entries):
+ * out[j][c] = (accumulate[j] ? out[j][c] : 0) + sum_{s < nslab[j]} ws[j][s*cols[j] + c], slabs summed
+ * in a fixed order.  Jobs are batched into as few launches as possible (a job whose output repeats an
+ * earlier job's output of the same launch starts a new launch, so accumulations keep their order). */
+int k3m_slab_reduce_batch(const float* const* ws, float* const* out, const int* nslab, const int* cols,
+                          const int* accumulate, int njobs, hipStream_t stream);
 
 /* Post-LN residual block tail (BertSelfOutput/BertOutput/BertBiOutput/BertImageEmbeddings,
  * vilbert_k3m.py:485-489, :528-532, :986-996, :2153-2161, LayerNorm :319-332):
@@ -95,9 +105,9 @@ int k3m_ln_bwd(const void* dy, const void* xhat, const float* rstd, const float*
                float* dgamma, float* dbeta, float* dxsum, int rows, int cols, float p_in, float p_out, uint64_t seed,
                uint64_t off_in, uint64_t off_out, int accumulate_res, float* ws, int dtype, hipStream_t stream);
 /* k3m_ln_bwd without the reduction: dres/dx written, the dgamma / dbeta / (want_sum) sum(dx)
- * column partials left as 3 arrays of k3m_ln_bwd_nslab(rows) slabs (array a at ws + a*nslab*cols)
- * for k3m_slab_reduce_batch. */
-int k3m_ln_bwd_nslab(int rows);
+ * column partials left as 3 arrays of nslab slabs (array a at ws + a*nslab*cols, nslab from
+ * k3m_ln_bwd_nslab) for k3m_slab_reduce_batch. */
+int k3m_ln_bwd_nslab(int rows, int* nslab);
 int k3m_ln_bwd_slabs(const void* dy, const void* xhat, const float* rstd, const float* gamma, void* dres, void* dx,
                      int rows, int cols, float p_in, float p_out, uint64_t seed, uint64_t off_in, uint64_t off_out,
                      int accumulate_res, int want_sum, float* ws, int dtype, hipStream_t stream);

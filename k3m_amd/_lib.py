@@ -34,6 +34,11 @@ SIGNATURES = {
     "k3m_colsum": [vp, i64, i32, i32, vp, i32, vp, i32, vp],
     "k3m_ln_fwd": [vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, f32, u64, u64, u64, i32, vp],
     "k3m_ln_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, u64, u64, u64, i32, vp, i32, vp],
+    "k3m_ln_bwd_nslab": [i32, vp],
+    "k3m_ln_bwd_slabs": [vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, u64, u64, u64, i32, i32, vp, i32, vp],
+    "k3m_colsum_nslab": [i32, vp],
+    "k3m_colsum_slabs": [vp, i64, i32, i32, vp, i32, vp],
+    "k3m_slab_reduce_batch": [vp, vp, vp, vp, vp, i32, vp],
     "k3m_embed_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, u64, u64, i32, vp],
     "k3m_embed_bwd": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp],
     "k3m_attn_fwd": [vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, i32, f32, f32, u64, u64, i32, vp],

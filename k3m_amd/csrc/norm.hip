@@ -101,10 +101,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 
 // Column-slab reductions.  The LayerNorm backward and the column sums leave one fp32 slab of
 // column partials per workgroup (ws[a][slab][c]); out_a[c] (+)= sum over slabs.  The slabs of MANY
-// such reductions are summed by ONE batched launch (k3m_slab_reduce_batch): the engine defers them
-// through a whole encoder block's backward and flushes before the block's gradients are handed to
-// the all-reduce (k3m_amd.ops.deferred_reductions), instead of two small launches after every
-// LayerNorm / bias gradient (~4.7 us each, 466 per bf16 step).  An in-kernel reduction (last
+// such reductions can be summed by ONE batched launch (k3m_slab_reduce_batch, up to SLAB_JOBS jobs);
+// k3m_ln_bwd / k3m_colsum issue their own reduction right after the producing kernel (one launch
+// for dgamma, dbeta and the fused bias gradient together).  An in-kernel reduction (last
 // arriving block sums, agent-scope hand-off) measured slower: its two acquire hops sit on the
 // critical path of every call (scripts/lab/norm_fused_inkernel_slab_reduce.hip.txt).
 // Each workgroup: 64 columns x 4 slab phases (phase p sums slabs p, p+4, ... with 8 loads in
@@ -463,7 +462,13 @@ extern "C" int k3m_ln_fwd(const void* x, const void* res, const float* gamma, co
   return 0;
 }
 
-extern "C" int k3m_ln_bwd_nslab(int rows) { return std::max(1, std::min(LN_BWD_BLOCKS, k3m_cdiv(rows, 4))); }
+static int ln_bwd_slab_count(int rows) { return std::max(1, std::min(LN_BWD_BLOCKS, k3m_cdiv(rows, 4))); }
+
+extern "C" int k3m_ln_bwd_nslab(int rows, int* nslab) {
+  K3M_ARG(nslab && rows >= 0);
+  *nslab = ln_bwd_slab_count(rows);
+  return 0;
+}
 
 extern "C" int k3m_ln_bwd_slabs(const void* dy, const void* xhat, const float* rstd, const float* gamma, void* dres,
                                 void* dx, int rows, int cols, float p_in, float p_out, uint64_t seed, uint64_t off_in,
@@ -471,7 +476,7 @@ extern "C" int k3m_ln_bwd_slabs(const void* dy, const void* xhat, const float* r
   K3M_ARG(dy && xhat && rstd && gamma && dres && dx && ws);
   K3M_ARG(cols % 256 == 0 && cols <= 1024 && rows >= 0);
   if (rows == 0) return 0;
-  const int nb = k3m_ln_bwd_nslab(rows);
+  const int nb = ln_bwd_slab_count(rows);
   DISPATCH_T(dtype, hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3(nb), dim3(256), 0, st, (const T*)dy, (const T*)xhat, rstd,
                                        gamma, (T*)dres, (T*)dx, ws, rows, cols, p_in, p_out, seed, off_in, off_out,
                                        acc_res, want_sum));
@@ -517,7 +522,7 @@ extern "C" int k3m_ln_bwd(const void* dy, const void* xhat, const float* rstd, c
   const int rc = k3m_ln_bwd_slabs(dy, xhat, rstd, gamma, dres, dx, rows, cols, p_in, p_out, seed, off_in, off_out,
                                   acc_res, dxsum != nullptr, ws, dtype, st);
   if (rc) return rc;
-  const int nb = k3m_ln_bwd_nslab(rows);
+  const int nb = ln_bwd_slab_count(rows);
   const float* wsa[3] = {ws, ws + (long long)nb * cols, ws + 2LL * nb * cols};
   float* outs[3] = {dgamma, dbeta, dxsum};
   const int ns[3] = {nb, nb, nb}, cs[3] = {cols, cols, cols}, acc[3] = {1, 1, 1};
@@ -550,12 +555,18 @@ extern "C" int k3m_embed_bwd(const int64_t* ids, const int64_t* tt, const void* 
   return 0;
 }
 
-extern "C" int k3m_colsum_nslab(int rows) { return std::max(1, std::min(K3M_COLSUM_SLABS, k3m_cdiv(rows, 64))); }
+static int colsum_slab_count(int rows) { return std::max(1, std::min(K3M_COLSUM_SLABS, k3m_cdiv(rows, 64))); }
+
+extern "C" int k3m_colsum_nslab(int rows, int* nslab) {
+  K3M_ARG(nslab && rows >= 0);
+  *nslab = colsum_slab_count(rows);
+  return 0;
+}
 
 extern "C" int k3m_colsum_slabs(const void* x, long long ld, int rows, int cols, float* ws, int dtype, hipStream_t st) {
   K3M_ARG(x && ws && rows >= 0 && cols >= 0);
   if (cols == 0) return 0;
-  const int chunks = k3m_colsum_nslab(rows);
+  const int chunks = colsum_slab_count(rows);
   const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && ld % 8 == 0 && cols % 8 == 0;
   if (vec) {
     DISPATCH_T(dtype, hipLaunchKernelGGL(colsum_vec_kernel<T>, dim3(k3m_cdiv(cols, 512), chunks), dim3(256), 0, st,
@@ -576,7 +587,7 @@ extern "C" int k3m_colsum(const void* x, long long ld, int rows, int cols, float
   if (rc) return rc;
   const float* wsa[1] = {ws};
   float* outs[1] = {out};
-  const int ns[1] = {k3m_colsum_nslab(rows)}, cs[1] = {cols}, acc[1] = {accumulate};
+  const int ns[1] = {colsum_slab_count(rows)}, cs[1] = {cols}, acc[1] = {accumulate};
   return k3m_slab_reduce_batch(wsa, outs, ns, cs, acc, 1, st);
 }
 

@@ -1,6 +1,7 @@
 """The C-ABI library loads and exports every symbol include/k3m_hip.h declares (no GPU calls)."""
 import os
 import re
+import subprocess
 
 import pytest
 
@@ -26,6 +27,20 @@ def test_library_exports_every_symbol():
     assert sorted(got) == declared()
     lib = _lib.load()
     assert lib is not None
+
+
+def dynamic_k3m_symbols(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], check=True, capture_output=True, text=True).stdout
+    return sorted({ln.split()[-1] for ln in out.splitlines() if re.search(r" T k3m_", ln)})
+
+
+def test_library_exports_nothing_undeclared():
+    """Every exported k3m_* function is declared in include/k3m_hip.h (no hidden entry points)."""
+    from k3m_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        from k3m_amd.build_lib import build
+        build()
+    assert dynamic_k3m_symbols(_lib.LIB_PATH) == declared()
 
 
 def declared_data():
