@@ -180,6 +180,10 @@ class Trainer(object):
         if lr_schedule == "warmup_linear_fp16" and lr_mult:
             raise NotImplementedError("the --fp16 schedule quirk is defined for the two-group optimizer only")
         self.runs = optimizer_runs(fp, weight_decay, lr_mult, frozen_names)
+        # the reference's parameter-group layout (checkpoint interchange): per-tensor groups when a
+        # pretrained model is loaded (lr_mult given, possibly empty), else the two AdamW groups
+        self.lr_mult = dict(lr_mult) if lr_mult is not None else None
+        self.frozen_names = tuple(frozen_names)
         self.excluded = sorted(set(frozen_names))
         nopt = max(a + n for a, n, _, _ in self.runs)
         assert nopt <= fp.segments["frozen"][0] + 4
@@ -195,9 +199,11 @@ class Trainer(object):
         # LambdaLR: the constructor sets lr * lambda(0); scheduler.step() after each optimizer step
         return self.lr * warmup_linear_lambda(self.global_step, self.warmup, self.t_total)
 
-    def run_lr(self, wd, mult):
-        if self.lr_schedule == "warmup_linear_fp16" and wd == 0.0:
-            # only param_groups[0] (the decay group) is re-set (:584); the others keep lr * lambda(0)
+    def run_lr(self, off, mult):
+        """lr of the run starting at flat offset ``off``.  Under the --fp16 schedule only
+        ``param_groups[0]`` — the decay group, i.e. the flat buffer's decay segment — is re-set
+        (:584); every other group keeps lr * lambda(0) (two-group layout only, see __init__)."""
+        if self.lr_schedule == "warmup_linear_fp16" and off >= self.engine.fp.segments["no_decay"][0]:
             return mult * self.lr * warmup_linear_lambda(0, self.warmup, self.t_total)
         return mult * self.current_lr()
 
@@ -215,11 +221,11 @@ class Trainer(object):
             sh = fp.data16[off:].data_ptr() if fp.data16 is not None else None
             if self.ADAMW is not None:   # torch.optim.AdamW (fine-tuning); zeroing below
                 L.call(self.ADAMW, fp.data[off:].data_ptr(), fp.grad[off:].data_ptr(), self.m[off:].data_ptr(),
-                       self.v[off:].data_ptr(), sh, n, self.run_lr(wd, mult), self.beta1, self.beta2, self.eps, wd,
+                       self.v[off:].data_ptr(), sh, n, self.run_lr(off, mult), self.beta1, self.beta2, self.eps, wd,
                        step, grad_scale, L.stream())
                 continue
             L.call("k3m_adamw_ex", fp.data[off:].data_ptr(), fp.grad[off:].data_ptr(), self.m[off:].data_ptr(),
-                   self.v[off:].data_ptr(), sh, n, self.run_lr(wd, mult), self.beta1, self.beta2, self.eps, wd, step,
+                   self.v[off:].data_ptr(), sh, n, self.run_lr(off, mult), self.beta1, self.beta2, self.eps, wd, step,
                    grad_scale, flags, L.stream())
         if zero_grad and self.ADAMW is not None:
             fp.grad.zero_()

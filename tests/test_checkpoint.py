@@ -125,3 +125,69 @@ def test_resume_from_tar_continues_training(tmp_path):
     np.testing.assert_allclose(got, ref, rtol=1e-5)
     d = float((tr2.engine.fp.data - ref_p).norm() / ref_p.norm())
     assert d < 1e-5, d
+
+
+def test_checkpoint_per_tensor_groups_round_trip(tmp_path):
+    """Pretrained-model layout (train_concap_struc.py:368-385): one group per requires_grad tensor in
+    named_parameters() order, lr x multiplier, --freeze names left out; moments land on the same
+    tensors after a round trip, and a two-group file is rejected instead of mis-mapped."""
+    from k3m_amd import checkpoint as C
+    from k3m_amd.params import is_frozen, is_no_decay
+    cfg = _tiny_cfg()
+    src = _fake_trainer(cfg, 5, step=3)
+    names = [n for n, _ in src.engine.fp.spec]
+    frozen = [names[3], names[10]]
+    src.lr_mult = {names[0]: 0.1, names[7]: 0.1}
+    src.frozen_names = tuple(frozen)
+    tar = str(tmp_path / "pt.tar")
+    C.save_checkpoint(src, tar_path=tar)
+    ck = torch.load(tar, map_location="cpu", weights_only=True)
+    pg = ck["optimizer_state_dict"]["param_groups"]
+    kept = [n for n in names if n not in frozen]
+    assert len(pg) == len(kept)
+    assert [g["params"] for g in pg] == [[i] for i in range(len(kept))]
+    for g, n in zip(pg, kept):
+        assert g["weight_decay"] == (0.0 if is_no_decay(n) else 0.01), n
+        assert abs(g["initial_lr"] - src.lr * src.lr_mult.get(n, 1.0)) < 1e-15, n
+    assert len(ck["scheduler_state_dict"]["base_lrs"]) == len(kept)
+    assert set(ck["optimizer_state_dict"]["state"]) == {i for i, n in enumerate(kept) if not is_frozen(n)}
+
+    dst = _fake_trainer(cfg, 6, step=0)
+    dst.lr_mult, dst.frozen_names = dict(src.lr_mult), tuple(frozen)
+    dst.engine.fp.grad = torch.zeros_like(dst.engine.fp.data)
+    assert C.load_checkpoint(dst, tar) == 3
+    fs, fd = src.engine.fp, dst.engine.fp
+    for n in kept:
+        if not is_frozen(n):
+            o, k = fs.offsets[n], fs.p[n].numel()
+            assert torch.equal(src.m[o:o + k], dst.m[o:o + k]), n
+    assert dst.lr == src.lr
+
+    two = _fake_trainer(cfg, 7, step=0)   # two-group optimizer cannot take the per-tensor file
+    two.engine.fp.grad = torch.zeros_like(two.engine.fp.data)
+    with pytest.raises(ValueError):
+        C.load_checkpoint(two, tar)
+
+
+def test_checkpoint_fused_adam_layout(tmp_path):
+    """--apex_fast branch (:413-418): apex FusedAdam state_dict — per-group step and
+    bias_correction=False, per-parameter exp_avg / exp_avg_sq only."""
+    from k3m_amd import checkpoint as C
+    cfg = _tiny_cfg()
+    src = _fake_trainer(cfg, 8, step=4)
+    src.optimizer = "fused_adam"
+    tar = str(tmp_path / "fa.tar")
+    C.save_checkpoint(src, tar_path=tar)
+    osd = torch.load(tar, map_location="cpu", weights_only=True)["optimizer_state_dict"]
+    assert all(g["step"] == 4 and g["bias_correction"] is False for g in osd["param_groups"])
+    assert set(next(iter(osd["state"].values()))) == {"exp_avg", "exp_avg_sq"}
+    dst = _fake_trainer(cfg, 9, step=0)
+    dst.optimizer = "fused_adam"
+    dst.engine.fp.grad = torch.zeros_like(dst.engine.fp.data)
+    assert C.load_checkpoint(dst, tar) == 4
+    from k3m_amd.params import is_frozen
+    fs = src.engine.fp
+    for n, _ in fs.spec:
+        if not is_frozen(n):
+            o, k = fs.offsets[n], fs.p[n].numel()
+            assert torch.equal(src.m[o:o + k], dst.m[o:o + k]) and torch.equal(src.v[o:o + k], dst.v[o:o + k]), n

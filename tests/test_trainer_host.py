@@ -153,3 +153,16 @@ def test_raw_tsv_records(tmp_path):
     r = rd[1]
     assert r[0] == "2" and r[2] == "k:v;" and r[6] == 1 and r[7].shape == (1, 4) and r[8].shape == (1, 2048)
     np.testing.assert_allclose(r[7][0], [0.1, 0.1, 799.9, 799.9], rtol=1e-6)
+
+
+def test_fp16_schedule_first_group_is_the_decay_segment():
+    """--fp16 schedule quirk (train_concap_struc.py:579-584): only param_groups[0] — the decay group —
+    follows warmup_linear; identified by the flat-buffer segment, so weight_decay=0 still trains."""
+    from k3m_amd.trainer import Trainer
+    fp = _fp(_cfg())
+    t = types.SimpleNamespace(lr_schedule="warmup_linear_fp16", lr=1e-3, warmup=10, t_total=100,
+                              warmup_proportion=0.1, global_step=50, engine=types.SimpleNamespace(fp=fp))
+    t.current_lr = lambda: Trainer.current_lr(t)
+    dec, nod = fp.segments["decay"][0], fp.segments["no_decay"][0]
+    assert Trainer.run_lr(t, dec, 1.0) > 0            # group 0: re-set every step
+    assert Trainer.run_lr(t, nod, 1.0) == 0.0         # other groups keep lr * lambda(0) = 0
