@@ -133,6 +133,44 @@ bool prefer_256x256(const K3mGemm& g) {
   return 2.0 * (double)w256 / 1.08 < (double)w128;
 }
 
+// Persistent x6 walk (gemm_x6p.hip) for the 256-row tiles: K3M_X6_PERSIST=0 restores one workgroup per
+// tile (A/B knob).
+const int kPersist = [] {
+  const char* e = std::getenv("K3M_X6_PERSIST");
+  return e ? std::atoi(e) : 1;
+}();
+
+int cu_count() {
+  static int n = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      return 256;
+    return cus;
+  }();
+  return n;
+}
+
+}  // namespace
+
+int k3m_x6_persistent_launch(const k3m_x6::GemmGroup& grp, bool t256, bool ak, bool bk, int cus, hipStream_t st);
+int k3m_x6_variant_launch(const K3mGemm& g, int variant, hipStream_t st);   // lab tiles (gemm_x6p.hip)
+namespace {
+const int kVariant = [] {
+  const char* e = std::getenv("K3M_X6_VARIANT");
+  return e ? std::atoi(e) : 0;
+}();
+}  // namespace
+
+namespace {
+// one GEMM as a persistent group of one
+int launch_x6_persistent_one(const K3mGemm& g, bool t256, bool ak, bool bk, hipStream_t st) {
+  k3m_x6::GemmGroup grp = {};
+  grp.g[0] = g;
+  grp.start[0] = 0;
+  grp.start[1] = (int)nblocks(g, 256, t256 ? 256 : 128);
+  grp.count = 1;
+  return k3m_x6_persistent_launch(grp, t256, ak, bk, cu_count(), st);
+}
 }  // namespace
 
 int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st);  // gemm_bf16.hip
@@ -160,8 +198,13 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
   // (2,304-8,192 rows) otherwise leave CUs idle
   int rc;
   if (vec && g.f32_algo == K3M_F32_SPLIT_BF16X6) {
-    if (g.splitk > 1 || nblocks(g, 256, 128) >= 200) {
-      if ((ak || !bk) && prefer_256x256(g)) {
+    const int vrc = kVariant ? k3m_x6_variant_launch(g, kVariant, st) : -1;
+    if (vrc >= 0) {
+      rc = vrc;
+    } else if (g.splitk > 1 || nblocks(g, 256, 128) >= 200) {
+      if (kPersist) {
+        rc = launch_x6_persistent_one(g, (ak || !bk) && prefer_256x256(g), ak, bk, st);
+      } else if ((ak || !bk) && prefer_256x256(g)) {
         // wave layout per operand layout (scripts/lab, best of passes): 4x2 for the forward (both
         // K-contiguous), 2x4 when B is MN-contiguous (dgrad, and the single-register-set loop for
         // the weight gradients)
@@ -271,7 +314,9 @@ extern "C" int k3m_gemm_grouped(const K3mGemm* gs, int count, hipStream_t st) {
   grp.start[live] = nb;
   grp.count = live;
   int rc;
-  if (t256) {
+  if (kPersist) {
+    rc = k3m_x6_persistent_launch(grp, t256, ak, bk, cu_count(), st);
+  } else if (t256) {
     if (ak && bk) rc = launch_grouped_epi<256, 4, 2, 16, true, true, true>(grp, g0.epilogue, st);
     else if (ak) rc = launch_grouped_epi<256, 2, 4, 16, true, false, true>(grp, g0.epilogue, st);
     else rc = launch_grouped_epi<256, 2, 4, 16, false, false, false>(grp, g0.epilogue, st);

@@ -208,9 +208,17 @@ namespace K3M_F32_NS {
 // acc[i][j][r] holds row (r&3) + 8*(r>>2) + 4*(lane>>5), col lane&31 of MFMA tile (i, j).
 // Split-K (splitk > 1): the block's slab ws[blockIdx.y] gets the raw sum (alpha/beta are applied
 // by the reduction kernel).
-template <int TBM, int TBN, int WM, int WN, int EPI, int CAP = 2 * (TBM + TBN) * BK>
+struct NoHook {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+// hook(): called once, after the first accumulator slice is in LDS and before any global store (the
+// persistent x6 kernel issues the next tile's loads there, when acc[0] is dead and the loads are
+// older than every store of this tile).
+template <int TBM, int TBN, int WM, int WN, int EPI, int CAP = 2 * (TBM + TBN) * BK, class Hook = NoHook>
 __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, float* smem,
-                                         const floatx16 (&acc)[TBM / WM / 32][TBN / WN / 32], int slice = -1) {
+                                         const floatx16 (&acc)[TBM / WM / 32][TBN / WN / 32], int slice = -1,
+                                         Hook hook = Hook()) {
   constexpr int FM = TBM / WM / 32, FN = TBN / WN / 32;
   constexpr int WCOLS = FN * 32, WS = WCOLS + 8, LPR = WCOLS / 8, RPP = 64 / LPR;
   static_assert(WM * WN * 32 * WS <= CAP, "epilogue staging exceeds the LDS tile");
@@ -239,6 +247,7 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, float
 #pragma unroll
       for (int r = 0; r < 16; ++r) wl[((r & 3) + 8 * (r >> 2) + 4 * kl) * WS + 32 * j + cl] = acc[i][j][r];
     __syncthreads();
+    if (i == 0) hook();
 #pragma unroll
     for (int ps = 0; ps < 32 / RPP; ++ps) {
       const int rr = ps * RPP + lr;

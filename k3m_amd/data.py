@@ -295,6 +295,8 @@ class RegionCollator(object):
         # forward then sizes its compacted head buffers without a device->host sync
         batch["_label_counts"] = (int((text[:, 3] >= 0).sum()) + int((pv[:, 3] >= 0).sum()),
                                   int(sum(int((s.image_label >= 1).sum()) for s in samples)))
+        # host copies of the PV spans: the driver-facing iterator yields these (no device->host copy)
+        batch["_index_host"] = (np.stack([s.index_p for s in samples]), np.stack([s.index_v for s in samples]))
         return batch, [s.item_id for s in samples]
 
 

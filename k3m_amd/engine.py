@@ -560,6 +560,30 @@ class K3MEngine(object):
         return sch
 
     # ------------------------------------------------------------ forward
+    def _verify_hint(self, hint, cnt):
+        """Check a host-side label-count hint against the device count without blocking: the count is
+        copied to pinned memory behind an event and compared once the event has completed (a later
+        forward, or check_hints(wait=True)); a mismatch raises — the head buffers were sized wrong."""
+        host = torch.empty((2,), dtype=torch.int32, pin_memory=True)
+        host.copy_(cnt, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        if not hasattr(self, "_hint_checks"):
+            self._hint_checks = []
+        self._hint_checks.append((tuple(hint), host, ev))
+        self.check_hints()
+
+    def check_hints(self, wait=False):
+        pend = getattr(self, "_hint_checks", [])
+        while pend and (wait or pend[0][2].query()):
+            hint, host, ev = pend.pop(0)
+            ev.synchronize()
+            got = (int(host[0]), int(host[1]))
+            if got != hint:
+                pend.clear()
+                raise RuntimeError("stale labelled-row count hint %s: the labels hold %s (labels edited after "
+                                   "collation, or a hand-built _label_counts)" % (hint, got))
+
     def forward(self, batch, train=True, noise=None, ent_neg=None, val_neg=None, seed=None, groups=1):
         """Runs the forward of the step; returns (losses dict of device tensors, ctx for backward).
 
@@ -810,20 +834,22 @@ class K3MEngine(object):
         # ---- heads on labelled rows only (unlabelled logits do not reach the loss or the gradients)
         losses = torch.zeros((4,), dtype=torch.float32, device=dev)   # mlm_t, mlm_pv, img, -
         nmax = BT + BP
-        idx_m = torch.empty((nmax,), dtype=torch.int32, device=dev)
-        lab_m = torch.empty((nmax,), dtype=torch.int64, device=dev)
-        sc_m = torch.empty((nmax,), dtype=torch.float32, device=dev)
-        sl_m = torch.empty((nmax,), dtype=torch.int32, device=dev)
+        # zero-filled: rows past the device count (a hint larger than the true count) gather row 0 with
+        # row_scale 0 and add nothing to any loss or gradient; a smaller hint is caught by _check_hints
+        idx_m = torch.zeros((nmax,), dtype=torch.int32, device=dev)
+        lab_m = torch.zeros((nmax,), dtype=torch.int64, device=dev)
+        sc_m = torch.zeros((nmax,), dtype=torch.float32, device=dev)
+        sl_m = torch.zeros((nmax,), dtype=torch.int32, device=dev)
         cnt = torch.zeros((2,), dtype=torch.int32, device=dev)
         L.call("k3m_compact_labels_ex", batch["lm_label_ids"].contiguous().data_ptr(), BT, 0, T, T, 0, 0,
                idx_m.data_ptr(), lab_m.data_ptr(), None, sc_m.data_ptr(), sl_m.data_ptr(), cnt.data_ptr(), L.stream())
         L.call("k3m_compact_labels_ex", batch["lm_label_ids_pv"].contiguous().data_ptr(), BP, 0, P, P, BT, 1,
                idx_m.data_ptr(), lab_m.data_ptr(), None, sc_m.data_ptr(), sl_m.data_ptr(), cnt.data_ptr(), L.stream())
         R1 = R - 1
-        idx_v = torch.empty((B * R1,), dtype=torch.int32, device=dev)
-        src_v = torch.empty((B * R1,), dtype=torch.int32, device=dev)
-        sc_v = torch.empty((B * R1,), dtype=torch.float32, device=dev)
-        sl_v = torch.empty((B * R1,), dtype=torch.int32, device=dev)
+        idx_v = torch.zeros((B * R1,), dtype=torch.int32, device=dev)
+        src_v = torch.zeros((B * R1,), dtype=torch.int32, device=dev)
+        sc_v = torch.zeros((B * R1,), dtype=torch.float32, device=dev)
+        sl_v = torch.zeros((B * R1,), dtype=torch.int32, device=dev)
         cnt_v = cnt[1:2]
         L.call("k3m_compact_labels_ex", batch["image_label"].contiguous().data_ptr(), B * R1, 1, R1, R, 1, 2,
                idx_v.data_ptr(), None, src_v.data_ptr(), sc_v.data_ptr(), sl_v.data_ptr(), cnt_v.data_ptr(),
@@ -831,6 +857,7 @@ class K3MEngine(object):
         hint = batch.get("_label_counts")
         if hint is not None:   # counted on the host when the batch was built (label_counts): no sync
             n_m, n_v = int(hint[0]), int(hint[1])
+            self._verify_hint((n_m, n_v), cnt)
         else:
             n_m, n_v = [int(x) for x in cnt.tolist()]   # host sync (labelled-row counts)
 

@@ -190,6 +190,16 @@ class Trainer(object):
         self.m = torch.zeros(nopt, dtype=torch.float32, device=fp.device)
         self.v = torch.zeros(nopt, dtype=torch.float32, device=fp.device)
         self.watch = LossWatch() if nan_check else None
+        self.dropout = True   # False: the step runs without dropout (model.eval() forward; parity runs)
+
+    def evaluate(self, batch, noise=None, ent_neg=None, val_neg=None):
+        """The validation forward of train_concap_struc.py:612-688 (model.eval(), no gradients): returns
+        the losses dict with ``loss`` = mlm_t + img * loss_img_weight + mlm_pv + lpm (:656-657)."""
+        out, _ = self.engine.forward(batch, train=False, noise=noise, ent_neg=ent_neg, val_neg=val_neg,
+                                     seed=self.global_step * self.accum_steps + self.micro)
+        out["loss"] = out["masked_lm_loss"] + out["masked_lm_loss_pv"] + out["loss_lpm"] + \
+            out["masked_img_loss"] * self.loss_img_weight
+        return out
 
     # ---------------------------------------------------------------- schedule
     def current_lr(self):
@@ -253,7 +263,7 @@ class Trainer(object):
         eng = self.engine
         if self.objective == 1:
             batch = objective1_labels(batch)
-        out, ctx = eng.forward(batch, train=True, noise=noise, ent_neg=ent_neg, val_neg=val_neg,
+        out, ctx = eng.forward(batch, train=self.dropout, noise=noise, ent_neg=ent_neg, val_neg=val_neg,
                                seed=self.global_step * self.accum_steps + self.micro)
         w = 1.0 / self.accum_steps
         out["loss"] = out["masked_lm_loss"] + out["masked_lm_loss_pv"] + out["loss_lpm"] + \

@@ -79,5 +79,5 @@ if __name__ == "__main__":
         sys.argv[3] if len(sys.argv) > 3 else "fp32"]
     for d in dts:
         for sh in SHAPES:
-            if only is None or sh[0] == only:
+            if only is None or only in sh[0]:
                 run(*sh, reps=reps, dtype=d)

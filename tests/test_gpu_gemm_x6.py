@@ -158,3 +158,49 @@ def test_grouped_matches_individual():
         res[grouped] = (gws, dxs)
     for a, b in zip(res[True][0] + res[True][1], res[False][0] + res[False][1]):
         assert torch.equal(a, b)
+
+
+_PERSIST_SCRIPT = r'''
+import sys, torch
+sys.path.insert(0, sys.argv[2])
+from k3m_amd import ops, _lib as L
+dev = torch.device("cuda")
+out = {}
+torch.manual_seed(5)
+# forward with bias+GELU (256x256 persistent walk, ragged M), dgrad with dGELU, split-K weight gradient,
+# a 256x128 problem and a grouped launch
+x = torch.randn(5000, 768, device=dev); w = torch.randn(3072, 768, device=dev) * 0.05; b = torch.randn(3072, device=dev)
+pre = torch.empty(5000, 3072, device=dev)
+out["fwd"] = ops.linear(x, w, b, epi=L.EPI_BIAS_GELU, aux=pre); out["pre"] = pre
+dy = torch.randn(5000, 3072, device=dev); aux = torch.randn(5000, 768, device=dev)
+out["dgrad"] = ops.linear_dgrad(dy, w, dgelu_aux=aux)
+gw = torch.ones(3072, 768, device=dev)
+ops.linear_wgrad(dy, x, gw); out["wgrad"] = gw
+x2 = torch.randn(2368, 1024, device=dev); w2 = torch.randn(1024, 1024, device=dev) * 0.05; b2 = torch.randn(1024, device=dev)
+out["t128"] = ops.linear(x2, w2, b2)
+with ops.grouped():
+    g1 = ops.linear(x2, w2, b2); g2 = ops.linear(x[:2304], w[:1024], b[:1024])
+out["g1"], out["g2"] = g1, g2
+torch.cuda.synchronize()
+torch.save({k: v.cpu() for k, v in out.items()}, sys.argv[1])
+'''
+
+
+def test_persistent_walk_bit_identical(tmp_path):
+    """The persistent x6 walk (gemm_x6p.hip, K3M_X6_PERSIST=1, default) computes every tile exactly as the
+    one-workgroup-per-tile kernels (K3M_X6_PERSIST=0): bit-identical C, aux, split-K sums and grouped
+    outputs (the knob is read at library load, so each setting runs in its own process)."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "persist_case.py"
+    script.write_text(_PERSIST_SCRIPT)
+    res = {}
+    for knob in ("0", "1"):
+        path = str(tmp_path / ("out%s.pt" % knob))
+        env = dict(os.environ, K3M_X6_PERSIST=knob)
+        subprocess.run([sys.executable, str(script), path, repo], check=True, env=env, timeout=240)
+        res[knob] = torch.load(path, weights_only=True)
+    for k in res["0"]:
+        assert torch.equal(res["0"][k], res["1"][k]), k
