@@ -36,6 +36,8 @@ import time
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
+# BASELINE.json "metric"; `value` is the whole-job aggregate over the n_gpus ranks (per_gpu_samples_s beside it)
+BASELINE_METRIC = "pretrain samples/sec/GPU (bert_base_6layer_6conect, bs=64) at 1/2/4/8 MI355X"
 PEAK_F32_MFMA = 157.3e12      # MI355X f32 MFMA dense peak (MI355X_MICROARCH.md)
 PEAK_BF16_MFMA = 2.5e15
 PEAK_F32_X6 = PEAK_BF16_MFMA / 6   # fp32 GEMM as 6 bf16 MFMA partial products (gemm_x6_tile.h)
@@ -76,8 +78,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
     ap.add_argument("--dtype", default=None, choices=["fp32", "bf16"], help="default: the config's")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=8)
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-batch", type=int, default=64, help="CPU baseline batch (the GPU workload's bs=64)")
+    ap.add_argument("--cpu-steps", type=int, default=1, help="timed CPU steps at --cpu-batch (after a bs=8 "
+                    "warm-up step and a bs=8 sample of 2 timed steps)")
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL) for real runs; gloo only to rehearse the "
                     "multi-rank path with several ranks sharing one GPU")
     ap.add_argument("--master-port", type=int, default=0)
@@ -191,7 +194,10 @@ def cpu_model():
 
 
 def cpu_baseline(cfg, shape, bsz, steps):
-    """Oracle (torch CPU fp32) fwd+bwd+AdamW on a bounded sample of the same workload; baseline only."""
+    """Oracle (torch CPU fp32) fwd+bwd+AdamW on a bounded sample of the same workload; baseline only.
+    Threads: this process's CPU share on the GPU box (OMP_NUM_THREADS, 16 per GPU there), not the
+    machine's nproc (reported beside it).  One bs=8 warm-up step, a bs=8 sample (2 timed steps), then
+    ``steps`` timed steps at ``bsz`` (the GPU workload's batch)."""
     import torch
     from oracle import k3m_oracle as O
     from k3m_amd.weights import init_values
@@ -200,41 +206,55 @@ def cpu_baseline(cfg, shape, bsz, steps):
     torch.set_num_threads(ncores)
     P = {k: torch.from_numpy(v).requires_grad_(True) for k, v in init_values(cfg, 0).items()}
     T, Pl, nbox = shape["T"], shape["P"], shape["nbox"]
-    batch = synthetic_batch(cfg, bsz, "cpu", seed=99, T=T, P=Pl, n_boxes=nbox, n_triples=shape["n_triples"],
-                            npv=shape["npv"])
-    noise = synthetic_noise(cfg, bsz, seed=1, T=T, P=Pl, R=nbox + 1)
-    NPV = batch["index_p"].shape[1]
-    nt = shape["n_triples"]
-    ent = torch.full((bsz, NPV, 2), -1, dtype=torch.int64)
-    val = torch.full((bsz, NPV, 2), -1, dtype=torch.int64)
-    for i in range(bsz):
-        for j in range(nt):
-            ent[i, j, 0] = (i + 1) % bsz if bsz > 1 else -1
-            ent[i, j, 1] = (i + 2) % bsz if bsz > 2 else -1
-            val[i, j, 0] = (j + 1) % nt
-            val[i, j, 1] = (j + 2) % nt
     state = {k: (torch.zeros_like(v), torch.zeros_like(v)) for k, v in P.items()}
 
-    def step(t):
-        out = O.forward(P, cfg, batch, noise, ent, val)
+    def make(b):
+        batch = synthetic_batch(cfg, b, "cpu", seed=99, T=T, P=Pl, n_boxes=nbox, n_triples=shape["n_triples"],
+                                npv=shape["npv"])
+        noise = synthetic_noise(cfg, b, seed=1, T=T, P=Pl, R=nbox + 1)
+        NPV = batch["index_p"].shape[1]
+        nt = shape["n_triples"]
+        ent = torch.full((b, NPV, 2), -1, dtype=torch.int64)
+        val = torch.full((b, NPV, 2), -1, dtype=torch.int64)
+        for i in range(b):
+            for j in range(nt):
+                ent[i, j, 0] = (i + 1) % b if b > 1 else -1
+                ent[i, j, 1] = (i + 2) % b if b > 2 else -1
+                val[i, j, 0] = (j + 1) % nt
+                val[i, j, 1] = (j + 2) % nt
+        return batch, noise, ent, val
+
+    tstep = [0]
+
+    def step(inp):
+        tstep[0] += 1
+        out = O.forward(P, cfg, *inp)
         out["loss"].backward()
         with torch.no_grad():
             for k, p in P.items():
                 if p.grad is None:
                     continue
                 m, v = state[k]
-                O.adamw_step(p.data, p.grad, m, v, t, 1e-4, 0.0 if ("bias" in k or "LayerNorm" in k) else 0.01)
+                O.adamw_step(p.data, p.grad, m, v, tstep[0], 1e-4, 0.0 if ("bias" in k or "LayerNorm" in k) else 0.01)
                 p.grad = None
 
-    step(1)
+    small = make(8)
+    step(small)
     t0 = time.perf_counter()
-    for t in range(steps):
-        step(t + 2)
+    for _ in range(2):
+        step(small)
+    dt8 = time.perf_counter() - t0
+    big = make(bsz) if bsz != 8 else small
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(big)
     dt = time.perf_counter() - t0
     return {"value": round(bsz * steps / dt, 4), "unit": "samples/s", "cores": ncores, "kind": "port",
-            "cpu_model": cpu_model(),
-            "sample": "oracle/k3m_oracle.py fwd+bwd+AdamW, fp32, bs=%d, %d timed steps after 1 warm-up, %.1f s "
-                      "(same shapes as the GPU workload; torch CPU, %d threads)" % (bsz, steps, dt, ncores)}
+            "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+            "bs8_samples_s": round(8 * 2 / dt8, 4),
+            "sample": "oracle/k3m_oracle.py fwd+bwd+AdamW, fp32, bs=%d, %d timed step(s) (%.1f s) after a bs=8 warm-up; "
+                      "bs=8: 2 timed steps %.1f s (same shapes as the GPU workload; torch CPU, %d threads = this "
+                      "process's CPU share; the machine has %d)" % (bsz, steps, dt, dt8, ncores, os.cpu_count() or 0)}
 
 
 def main():
@@ -269,7 +289,7 @@ def main():
     tr = Trainer(cfg, dev, lr=1e-4, warmup_steps=max(1, (args.steps + args.warmup) // 10),
                  total_steps=10 * (args.steps + args.warmup), seed=1234, init=True, dtype=dtype)
     if world > 1:
-        ddp = GradAllReducer(tr.engine.fp)
+        ddp = GradAllReducer(tr.engine.fp, comm_dtype=torch.bfloat16 if dtype == "bf16" else None)
         ddp.broadcast_params(tr.engine.fp)
         tr.ddp = ddp
     batch = synthetic_batch(cfg, B, dev, seed=1234 + rank, T=shape["T"], P=shape["P"], n_boxes=shape["nbox"],
@@ -321,7 +341,7 @@ def main():
     co_flops = 3.0 * coattn_fwd_flops(T, P, R) * B
     co_ms = cprobe.total_ms() / args.steps if cprobe.events else None
     res = {
-        "metric": "pretrain samples/sec (whole job; bert_base_6layer_6conect, bs=%d/GPU)" % B,
+        "metric": BASELINE_METRIC,
         "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": dtype, "data": "synthetic (SURVEY §8(d): random token ids, %dx2048 region feats, %d PV triples)" % (
@@ -355,6 +375,16 @@ def main():
         res["per_rank_s"] = [round(x, 4) for x in per_rank]
         res["backend"] = args.backend
         res["world_size_seen"] = dist.get_world_size()
+        tm = tr.ddp.timing(last=args.steps)
+        if tm is not None:
+            # rank 0's view: end of its last all-reduce minus end of its backward, averaged over the timed
+            # steps (0 = fully hidden behind the backward); busy = time the comm stream spent in buckets
+            res["allreduce_exposed_ms"] = round(tm["allreduce_exposed_ms"], 3)
+            res["allreduce_busy_ms"] = round(tm["allreduce_busy_ms"], 3)
+            res["allreduce_buckets_per_step"] = tm["buckets_per_step"]
+            res["allreduce_dtype"] = tm["comm_dtype"]
+            res["grad_bytes_per_rank"] = int(sum(b - a for blk in tr.ddp.blocks.values() for a, b in blk) *
+                                             (2 if tm["comm_dtype"] == "bf16" else 4))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             res["cpu_baseline"] = cpu_baseline(cfg, shape, args.cpu_batch, args.cpu_steps)

@@ -32,7 +32,7 @@ NAMES = ["cls.predictions.transform.dense.weight", "struc_w1.weight", "score_sel
          "v_embeddings.image_embeddings.weight"]
 
 
-def _worker(rank, world, port, backend, batch_size, out):
+def _worker(rank, world, port, backend, batch_size, out, dtype="fp32"):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -52,7 +52,7 @@ def _worker(rank, world, port, backend, batch_size, out):
     cfg.hidden_dropout_prob = cfg.attention_probs_dropout_prob = 0.0
     cfg.v_hidden_dropout_prob = cfg.v_attention_probs_dropout_prob = 0.0
     B = batch_size
-    tr = Trainer(cfg, dev, lr=1e-3, warmup_steps=0, total_steps=10, seed=5)
+    tr = Trainer(cfg, dev, lr=1e-3, warmup_steps=0, total_steps=10, seed=5, dtype=dtype)
     eng = tr.engine
     batch = synthetic_batch(cfg, B, dev, seed=100 + rank)
     noise = {k: v.to(dev) for k, v in synthetic_noise(cfg, B, seed=200 + rank).items()}
@@ -76,7 +76,7 @@ def _worker(rank, world, port, backend, batch_size, out):
     local_abs = float(eng.fp.grad.double().abs().sum())
     eng.fp.grad.zero_()
 
-    ddp = GradAllReducer(eng.fp)
+    ddp = GradAllReducer(eng.fp, comm_dtype=torch.bfloat16 if dtype == "bf16" else None)
     order = []
     orig = ddp._launch
 
@@ -111,6 +111,8 @@ def main():
     ap.add_argument("--world", type=int, default=2)
     ap.add_argument("--backend", default="gloo")
     ap.add_argument("--batch", type=int, default=2)
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="bf16: bf16 encoder and bf16 gradient buckets (reduced-gradient tolerance 1e-2)")
     a = ap.parse_args()
     import torch
     import torch.multiprocessing as mp
@@ -119,11 +121,11 @@ def main():
     port = s.getsockname()[1]
     s.close()
     out = tempfile.mkdtemp(prefix="k3m_ddp_")
-    mp.spawn(_worker, args=(a.world, port, a.backend, a.batch, out), nprocs=a.world, join=True)
+    mp.spawn(_worker, args=(a.world, port, a.backend, a.batch, out, a.dtype), nprocs=a.world, join=True)
     R = [torch.load(os.path.join(out, "r%d.pt" % r), weights_only=True) for r in range(a.world)]
     sched = R[0]["schedule"]
     expected = [["head", 0]] + [[k, i] for k, i in reversed(sched)] + [["emb", 0]]
-    res = {"world": a.world, "backend": a.backend, "world_seen": R[0]["world_seen"],
+    res = {"world": a.world, "backend": a.backend, "dtype": a.dtype, "world_seen": R[0]["world_seen"],
            "order_ok": all(r["order"] == expected for r in R), "order_rank0": R[0]["order"][:6] + ["..."]}
     worst = 0.0
     for n in NAMES:
@@ -139,8 +141,12 @@ def main():
     abs_scale = sum(r["local_abs"] for r in R) + 1e-12
     res["checksum_rel_err"] = max(abs(r["reduced_sum"] - want_sum) / abs_scale for r in R)
     res["params_equal_after_step"] = all(r["psum"] == R[0]["psum"] and r["pabs"] == R[0]["pabs"] for r in R)
-    res["ok"] = bool(res["order_ok"] and worst < 1e-5 and res["ranks_bitwise_equal"] and
-                     res["checksum_rel_err"] < 1e-6 and res["params_equal_after_step"] and
+    # fp32 buckets: the sum is exact to fp32 rounding; bf16 buckets round each rank's gradient and the
+    # partial sums to 8 significant bits (2^-8 relative per rounding, a few roundings per element)
+    tol, ctol = (1e-5, 1e-6) if a.dtype == "fp32" else (2e-2, 1e-2)
+    res["tolerance"] = tol
+    res["ok"] = bool(res["order_ok"] and worst < tol and res["ranks_bitwise_equal"] and
+                     res["checksum_rel_err"] < ctol and res["params_equal_after_step"] and
                      res["world_seen"] == a.world)
     print(json.dumps(res), flush=True)
     sys.exit(0 if res["ok"] else 1)

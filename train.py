@@ -242,7 +242,7 @@ def main(argv=None):
         logger.info("Successfully loaded model checkpoint ...")
     if distributed:
         from k3m_amd.ddp import GradAllReducer
-        trainer.ddp = GradAllReducer(fp)
+        trainer.ddp = GradAllReducer(fp, comm_dtype=torch.bfloat16 if mixed else None)
         trainer.ddp.broadcast_params(fp)
     if parity is not None:
         trainer.dropout = False
