@@ -101,9 +101,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 
 // Column-slab reductions.  The LayerNorm backward and the column sums leave one fp32 slab of
 // column partials per workgroup (ws[a][slab][c]); out_a[c] (+)= sum over slabs.  The slabs of MANY
-// such reductions can be summed by ONE batched launch (k3m_slab_reduce_batch, up to SLAB_JOBS jobs);
-// k3m_ln_bwd / k3m_colsum issue their own reduction right after the producing kernel (one launch
-// for dgamma, dbeta and the fused bias gradient together).  An in-kernel reduction (last
+// such reductions are summed by ONE batched launch (k3m_slab_reduce_batch, up to SLAB_JOBS jobs per
+// launch): the engine's backward calls the _slabs forms and flushes the collected jobs once per
+// encoder block, before the block is handed to the all-reduce (k3m_amd.ops.deferred_reductions);
+// k3m_ln_bwd / k3m_colsum are the one-call forms (their own reduction right after the producer).  An in-kernel reduction (last
 // arriving block sums, agent-scope hand-off) measured slower: its two acquire hops sit on the
 // critical path of every call (scripts/lab/norm_fused_inkernel_slab_reduce.hip.txt).
 // Each workgroup: 64 columns x 4 slab phases (phase p sums slabs p, p+4, ... with 8 loads in

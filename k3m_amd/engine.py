@@ -494,6 +494,9 @@ class K3MEngine(object):
         fp = self.fp = FlatParams(cfg, self.device, bf16_shadow=(dtype == "bf16"))
         self.base_seed = int(seed)
         self.step_count = 0
+        # tests: keep copies of the labelled-row MLM logits and masked-region logits of each forward
+        # (out["mlm_logits"] rows in compaction order — text rows, then PV rows, row-major; out["img_logits"])
+        self.capture_logits = False
         c = cfg
         assert getattr(c, "fixed_t_layer", 0) == 0 and getattr(c, "fixed_v_layer", 0) == 0
         assert not getattr(c, "in_batch_pairs", False) and not getattr(c, "fast_mode", False)
@@ -874,6 +877,8 @@ class K3MEngine(object):
         E = fp.p["embeddings.word_embeddings.weight"] if self.dtype != "bf16" else fp.p16(
             "embeddings.word_embeddings.weight")
         logits = ops.linear(self._lo(hl), E, fp.p["cls.predictions.bias"], out_dtype=torch.float32)
+        if self.capture_logits:   # the CE kernel overwrites the logits with their gradient
+            captured = {"mlm_logits": logits.clone()}
         lr_m = torch.empty((n_m,), dtype=torch.float32, device=dev)
         L.call("k3m_ce_fwd_bwd", logits.data_ptr(), V, lab_m.data_ptr(), sc_m.data_ptr(), n_m, V, lr_m.data_ptr(),
                L.stream())
@@ -893,6 +898,8 @@ class K3MEngine(object):
         if n_v:
             ops.ln_fwd(hv1, None, self.img_ln.g, self.img_ln.b, hlv, xh_iv, rs_iv)
         lv = self.img_dec.fwd(hlv)
+        if self.capture_logits:
+            captured["img_logits"] = lv.clone()
         tgt = batch["image_target"].reshape(B * R1, Cv).contiguous()
         lr_v = torch.empty((n_v,), dtype=torch.float32, device=dev)
         L.call("k3m_kl_fwd_bwd", lv.data_ptr(), Cv, tgt.data_ptr(), Cv, src_v.data_ptr(), sc_v.data_ptr(), n_v, Cv,
@@ -915,6 +922,8 @@ class K3MEngine(object):
             "pooled_t": pooled_t, "pooled_pv": pooled_pv, "pooled_v": pooled_v,
         }
         out["loss"] = losses[0:1] + losses[1:2] + losses[2:3] + lpm
+        if self.capture_logits:
+            out.update(captured)
         ctx["batch"] = batch
         return out, ctx
 
@@ -922,7 +931,19 @@ class K3MEngine(object):
     def backward(self, ctx, w_mlm=1.0, w_img=1.0, w_lpm=1.0, grad_ready=None):
         """Backward of  w_mlm*(mlm_t + mlm_pv) + w_img*img + w_lpm*lpm  (train_concap_struc.py:533).
         Parameter gradients are ACCUMULATED into self.fp.grad.  grad_ready(kind, index) is called as
-        soon as the gradients of an encoder block are final (DDP bucket hook)."""
+        soon as the gradients of an encoder block are final (DDP bucket hook).
+
+        The LayerNorm / bias-gradient slab reductions are batched (ops.deferred_reductions): flushed
+        right before each grad_ready hand-off (so the all-reduce sees final gradients) and at the end."""
+        with ops.deferred_reductions() as dr:
+            hook = None
+            if grad_ready is not None:
+                def hook(kind, index):
+                    dr.flush()
+                    grad_ready(kind, index)
+            self._backward(ctx, w_mlm, w_img, w_lpm, hook)
+
+    def _backward(self, ctx, w_mlm=1.0, w_img=1.0, w_lpm=1.0, grad_ready=None):
         c = self.cfg
         fp = self.fp
         dev = self.device

@@ -222,8 +222,81 @@ def linear_wgrad(dy, x, gW, gb=None, alpha=1.0):
             colsum(dy, gb, accumulate=True, alpha=alpha)
 
 
+# ------------------------------------------------------------------ deferred slab reductions
+# The LayerNorm backward and the bias-gradient column sums leave fp32 slabs of column partials; inside
+# deferred_reductions() those slabs are summed by ONE k3m_slab_reduce_batch launch per flush (the engine
+# flushes each encoder block before handing it to the all-reduce) instead of one small reduction launch
+# after every producer (~230 per step).  Workspaces stay referenced until their flush.
+_deferred = None
+
+
+class _Deferred(object):
+    def __init__(self):
+        self.jobs = []      # (ws pointer, out pointer, nslab, cols, accumulate)
+        self.keep = []      # workspaces referenced until the flush
+        self.stream = torch.cuda.current_stream() if torch.cuda.is_available() else None
+
+    def active_here(self):
+        return self.stream is not None and torch.cuda.current_stream() == self.stream
+
+    def add(self, ws_ptr, out, nslab, cols, accumulate=1):
+        self.jobs.append((ws_ptr, ptr(out), nslab, cols, accumulate))
+
+    def flush(self):
+        if not self.jobs:
+            return
+        import ctypes as C
+        n = len(self.jobs)
+        ws = (C.c_void_p * n)(*[j[0] for j in self.jobs])
+        out = (C.c_void_p * n)(*[j[1] for j in self.jobs])
+        ns = (C.c_int * n)(*[j[2] for j in self.jobs])
+        cs = (C.c_int * n)(*[j[3] for j in self.jobs])
+        acc = (C.c_int * n)(*[j[4] for j in self.jobs])
+        call("k3m_slab_reduce_batch", C.cast(ws, C.c_void_p), C.cast(out, C.c_void_p), C.cast(ns, C.c_void_p),
+             C.cast(cs, C.c_void_p), C.cast(acc, C.c_void_p), n, stream())
+        self.jobs = []
+        self.keep = []
+
+
+class deferred_reductions(object):
+    """Context: slab reductions of ln_bwd / colsum on the current stream are batched until flush()."""
+
+    def __enter__(self):
+        global _deferred
+        self.prev = _deferred
+        _deferred = self.d = _Deferred()
+        return self.d
+
+    def __exit__(self, *exc):
+        global _deferred
+        try:
+            if exc[0] is None:
+                self.d.flush()
+        finally:
+            _deferred = self.prev
+        return False
+
+
+def _nslab(fn, rows):
+    import ctypes as C
+    v = C.c_int(0)
+    call(fn, rows, C.byref(v))
+    return v.value
+
+
+DEFER = os.environ.get("K3M_DEFER_REDUCE", "1") != "0"   # A/B knob
+
+
 def colsum(x, out, accumulate=True, alpha=1.0):
     rows, cols = x.shape
+    if DEFER and _deferred is not None and alpha == 1.0 and accumulate and rows > 0 and cols > 0 and \
+            _deferred.active_here():
+        ns = _nslab("k3m_colsum_nslab", rows)
+        ws = torch.empty((ns * cols,), dtype=torch.float32, device=x.device)
+        call("k3m_colsum_slabs", ptr(x), _ld(x), rows, cols, ptr(ws), dt(x), stream())
+        _deferred.keep.append(ws)
+        _deferred.add(ptr(ws), out, ns, cols)
+        return
     ws = torch.empty(((256 + 16) * cols,), dtype=torch.float32, device=x.device)
     if alpha == 1.0:
         call("k3m_colsum", ptr(x), _ld(x), rows, cols, ptr(out), int(accumulate), ptr(ws), dt(x), stream())
@@ -254,6 +327,18 @@ def ln_bwd(dy, xhat, rstd, gamma, dres, dx, dgamma, dbeta, p_in=0.0, p_out=0.0, 
     """dxsum: optional fp32 [cols] that the column sums of dx are accumulated into (the bias
     gradient of the Linear whose output fed this LayerNorm)."""
     rows, cols = dy.shape
+    if DEFER and _deferred is not None and rows > 0 and _deferred.active_here():
+        ns = _nslab("k3m_ln_bwd_nslab", rows)
+        ws = torch.empty((3 * ns * cols,), dtype=torch.float32, device=dy.device)
+        call("k3m_ln_bwd_slabs", ptr(dy), ptr(xhat), ptr(rstd), ptr(gamma), ptr(dres), ptr(dx), rows, cols, p_in,
+             p_out, seed, off_in, off_out, int(acc_res), int(dxsum is not None), ptr(ws), dt(dy), stream())
+        _deferred.keep.append(ws)
+        base, step = ptr(ws), ns * cols * 4
+        _deferred.add(base, dgamma, ns, cols)
+        _deferred.add(base + step, dbeta, ns, cols)
+        if dxsum is not None:
+            _deferred.add(base + 2 * step, dxsum, ns, cols)
+        return
     ws = torch.empty((3 * (LN_BWD_SLABS + 16) * cols,), dtype=torch.float32, device=dy.device)
     call("k3m_ln_bwd", ptr(dy), ptr(xhat), ptr(rstd), ptr(gamma), ptr(dres), ptr(dx), ptr(dgamma), ptr(dbeta),
          ptr(dxsum), rows, cols, p_in, p_out, seed, off_in, off_out, int(acc_res), ptr(ws), dt(dy), stream())

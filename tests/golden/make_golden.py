@@ -225,6 +225,14 @@ def run_case(name, row_ids, data_seed, weight_seed, noise_seed, neg_seed, mode=1
         return r
 
     K.F.gumbel_softmax = fake_gumbel
+    cap = {}
+    real_cls_forward = model.cls.forward
+
+    def cls_capture(*a, **kw):   # BertPreTrainingHeads.forward (vilbert_k3m.py:1875-1909): keep the logits
+        r = real_cls_forward(*a, **kw)
+        cap["t"], cap["v"], cap["pv"], cap["nsp"] = r[0].detach(), r[1].detach(), r[2].detach(), r[6].detach()
+        return r
+    model.cls.forward = cls_capture
     random.seed(neg_seed)
     K.random.sample = rec_sample
     tb = {k: torch.from_numpy(np.asarray(v)) for k, v in batch.items()}
@@ -276,6 +284,26 @@ def run_case(name, row_ids, data_seed, weight_seed, noise_seed, neg_seed, mode=1
         if g is None:
             g = torch.zeros(tuple(params[n].shape))
         res["grad_slice/" + n] = (g[:4] if g.dim() == 2 else g[:256]).numpy()
+    # logits (north_star "logits"): MLM rows at the labelled positions, text rows then PV rows in
+    # row-major order (ignore_index -1), as 256 fixed vocabulary columns + the label's logit + the row's
+    # logsumexp (which pins the whole row's softmax); region logits of the masked regions (image_label
+    # == 1) over all classes, row 0 (the global region) dropped as the loss does (:2744)
+    V = cap["t"].shape[-1]
+    lt = cap["t"].reshape(-1, V)[torch.from_numpy(np.asarray(batch["lm_label_ids"]).reshape(-1) != -1)]
+    lp = cap["pv"].reshape(-1, V)[torch.from_numpy(np.asarray(batch["lm_label_ids_pv"]).reshape(-1) != -1)]
+    lab = np.concatenate([np.asarray(batch["lm_label_ids"]).reshape(-1), np.asarray(batch["lm_label_ids_pv"]).reshape(-1)])
+    lab = lab[lab != -1]
+    rows_m = torch.cat([lt, lp]).double()
+    cols = np.unique(np.concatenate([np.arange(8), np.arange(100, 108), [131, 132],
+                                     np.random.default_rng(2024).choice(V, 230, replace=False)]))[:256]
+    res["logit/mlm_cols"] = cols.astype(np.int64)
+    res["logit/mlm_rows"] = rows_m[:, torch.from_numpy(cols)].float().numpy()
+    res["logit/mlm_label"] = rows_m[torch.arange(len(lab)), torch.from_numpy(lab)].float().numpy()
+    res["logit/mlm_lse"] = torch.logsumexp(rows_m, 1).float().numpy()
+    pv_ = cap["v"][:, 1:]
+    res["logit/img_rows"] = pv_.reshape(-1, pv_.shape[-1])[
+        torch.from_numpy(np.asarray(batch["image_label"]).reshape(-1) == 1)].numpy()
+    res["logit/nsp"] = cap["nsp"].numpy()
     for k, v in batch.items():
         res["in/" + k] = np.asarray(v)
     path = os.path.join(HERE, "golden_%s.npz" % name)

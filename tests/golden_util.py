@@ -76,3 +76,33 @@ def ft_noise(g):
         shapes = [("v", (B, R, 3, 1024)), ("t", (B, T, 3, 768)), ("pv", (B, P, 3, 768))]
         out.append({k: torch.from_numpy((-np.log(rng.standard_exponential(sh))).astype(np.float32)) for k, sh in shapes})
     return out
+
+
+# ---------------------------------------------------------------- logits (north_star "logits")
+def check_logits(g, mlm_rows, img_rows, rtol, what="", mean_rtol=None):
+    """Compare labelled-row MLM logits (text rows then PV rows, row-major; [n, V]) and masked-region logits
+    ([n_v, Cv]) with the fixture's logit record (make_golden.py): the 256 recorded vocabulary columns,
+    each row's label logit and logsumexp, and every region class.  Tolerance: rtol of each row's
+    max |logit| (absolute per row)."""
+    mlm_rows = np.asarray(mlm_rows, np.float64)
+    img_rows = np.asarray(img_rows, np.float64)
+    assert mlm_rows.shape[0] == g["logit/mlm_rows"].shape[0], (what, mlm_rows.shape, g["logit/mlm_rows"].shape)
+    assert img_rows.shape == g["logit/img_rows"].shape, (what, img_rows.shape, g["logit/img_rows"].shape)
+    cols = g["logit/mlm_cols"]
+    scale = np.abs(g["logit/mlm_rows"]).max(1, keepdims=True) + 1e-6
+    d = np.abs(mlm_rows[:, cols] - g["logit/mlm_rows"]) / scale
+    np.testing.assert_array_less(d, rtol, err_msg=what + " mlm")
+    if mean_rtol is not None:
+        assert d.mean() < mean_rtol, (what, float(d.mean()))
+    m = mlm_rows.max(1)
+    lse = m + np.log(np.exp(mlm_rows - m[:, None]).sum(1))
+    np.testing.assert_allclose(lse, g["logit/mlm_lse"], rtol=rtol, atol=rtol, err_msg=what + " lse")
+    return img_rows, scale
+
+
+def check_img_logits(g, img_rows, rtol, what="", mean_rtol=None):
+    sc = np.abs(g["logit/img_rows"]).max(1, keepdims=True) + 1e-6
+    d = np.abs(np.asarray(img_rows, np.float64) - g["logit/img_rows"]) / sc
+    np.testing.assert_array_less(d, rtol, err_msg=what + " img")
+    if mean_rtol is not None:
+        assert d.mean() < mean_rtol, (what, float(d.mean()))

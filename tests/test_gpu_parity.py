@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 import torch
 
-from golden_util import CASES, load_case, case_config, case_batch, case_noise
+from golden_util import CASES, load_case, case_config, case_batch, case_noise, check_logits, check_img_logits
 
 pytestmark = pytest.mark.gpu
 
@@ -42,13 +42,20 @@ def test_engine_matches_reference_golden(dev, case):
     eng = engine_for(cfg, int(g["weight_seed"]), dev)
     batch = {k: v.to(dev) for k, v in case_batch(g).items()}
     noise = {k: v.to(dev) for k, v in case_noise(g).items()}
-    out, ctx = eng.forward(batch, train=False, noise=noise, ent_neg=torch.from_numpy(g["ent_neg"]),
-                           val_neg=torch.from_numpy(g["val_neg"]))
+    eng.capture_logits = True
+    try:
+        out, ctx = eng.forward(batch, train=False, noise=noise, ent_neg=torch.from_numpy(g["ent_neg"]),
+                               val_neg=torch.from_numpy(g["val_neg"]))
+    finally:
+        eng.capture_logits = False
     eng.backward(ctx)
     torch.cuda.synchronize()
     got = np.array([float(out[k]) for k in ("masked_lm_loss", "masked_img_loss", "masked_lm_loss_pv", "loss_lpm",
                                            "next_sentence_loss", "loss")])
     np.testing.assert_allclose(got, g["losses"], rtol=1e-3, atol=1e-4)
+    # logits of the labelled MLM rows and the masked regions (north_star "logits ... within 1e-3")
+    check_logits(g, out["mlm_logits"].cpu().numpy(), g["logit/img_rows"], 1e-3, case)
+    check_img_logits(g, out["img_logits"].cpu().numpy(), 1e-3, case)
     np.testing.assert_allclose(out["c_initial"].cpu().numpy(), g["c_initial"], rtol=1e-3, atol=1e-4)
     np.testing.assert_allclose(out["c_final"].cpu().numpy(), g["c_final"], rtol=1e-3, atol=1e-4)
     G = eng.fp.g
@@ -100,6 +107,8 @@ BF16_LOSS_RTOL = 1e-2
 BF16_GRAD_COS = 0.98
 BF16_GRAD_NORM_RTOL = 3e-2
 BF16_GLOBAL_COS = 0.995
+BF16_LOGIT_RTOL = 0.2
+BF16_LOGIT_MEAN = 1e-2
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -109,10 +118,18 @@ def test_bf16_engine_close_to_reference_golden(dev, case):
     eng = engine_for(cfg, int(g["weight_seed"]), dev, dtype="bf16")
     batch = {k: v.to(dev) for k, v in case_batch(g).items()}
     noise = {k: v.to(dev) for k, v in case_noise(g).items()}
-    out, ctx = eng.forward(batch, train=False, noise=noise, ent_neg=torch.from_numpy(g["ent_neg"]),
-                           val_neg=torch.from_numpy(g["val_neg"]))
+    eng.capture_logits = True
+    try:
+        out, ctx = eng.forward(batch, train=False, noise=noise, ent_neg=torch.from_numpy(g["ent_neg"]),
+                               val_neg=torch.from_numpy(g["val_neg"]))
+    finally:
+        eng.capture_logits = False
     eng.backward(ctx)
     torch.cuda.synchronize()
+    # bf16 encoder: every logit within BF16_LOGIT_RTOL of its row's max |logit|, mean error BF16_LOGIT_MEAN
+    check_logits(g, out["mlm_logits"].cpu().numpy(), g["logit/img_rows"], BF16_LOGIT_RTOL, case + " bf16",
+                 mean_rtol=BF16_LOGIT_MEAN)
+    check_img_logits(g, out["img_logits"].cpu().numpy(), BF16_LOGIT_RTOL, case + " bf16", mean_rtol=BF16_LOGIT_MEAN)
     got = np.array([float(out[k]) for k in ("masked_lm_loss", "masked_img_loss", "masked_lm_loss_pv", "loss_lpm",
                                            "next_sentence_loss", "loss")])
     rel = np.abs(got - g["losses"]) / np.maximum(np.abs(g["losses"]), 1e-3)

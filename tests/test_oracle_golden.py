@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 import torch
 
-from golden_util import CASES, load_case, case_config, case_batch, case_noise
+from golden_util import CASES, load_case, case_config, case_batch, case_noise, check_logits, check_img_logits
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -22,6 +22,14 @@ def test_oracle_matches_reference(case):
     np.testing.assert_allclose(got, g["losses"], rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(out["c_initial"].detach().numpy(), g["c_initial"], rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(out["c_final"].detach().numpy(), g["c_final"], rtol=1e-4, atol=1e-5)
+    b = case_batch(g)
+    V = out["logits_t"].shape[-1]
+    rows = torch.cat([out["logits_t"].reshape(-1, V)[b["lm_label_ids"].reshape(-1) != -1],
+                      out["logits_pv"].reshape(-1, V)[b["lm_label_ids_pv"].reshape(-1) != -1]]).detach()
+    check_logits(g, rows.numpy(), g["logit/img_rows"], 1e-5, case)
+    lv = out["logits_v"].detach()
+    lv = lv[:, 1:] if lv.shape[1] == b["image_label"].shape[1] + 1 else lv
+    check_img_logits(g, lv.reshape(-1, lv.shape[-1])[b["image_label"].reshape(-1) == 1].numpy(), 1e-5, case)
     for k in g:
         if k.startswith("grad_full/") or k.startswith("grad_slice/"):
             n = k.split("/", 1)[1]
