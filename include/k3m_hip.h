@@ -67,6 +67,11 @@ typedef struct K3mGemm {
   int f32_algo;          /* fp32 operands: K3M_F32_SPLIT_BF16X6 (0, default) or K3M_F32_MFMA_F32 */
 } K3mGemm;
 int k3m_gemm(const K3mGemm* g, hipStream_t stream);
+/* OR-ed into K3mGemm.epilogue of a split-K GEMM (splitk > 1, epilogue NONE): the kernel writes its fp32
+ * slabs (ws[slice][m][n], raw sums) and returns without reducing them — C is untouched.  The caller
+ * reduces them later with k3m_slab_reduce_batch (nslab = splitk, cols = m*n, requires ldc == n,
+ * alpha == 1; the engine batches these with the LayerNorm / bias slabs of a whole encoder block). */
+#define K3M_GEMM_SLABS_ONLY 0x100
 /* Up to 8 INDEPENDENT problems in one launch (no problem may read another's output).  When all share
  * one kernel template (fp32 operands on the bf16x6 path, same a_trans / b_trans / epilogue, 16-B
  * aligned) they run as one grid of 256x128 tiles — the co-attention blocks' six small GEMMs per

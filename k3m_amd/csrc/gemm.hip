@@ -173,12 +173,16 @@ int launch_x6_persistent_one(const K3mGemm& g, bool t256, bool ak, bool bk, hipS
 }
 }  // namespace
 
-int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st);  // gemm_bf16.hip
-int k3m_gemm_bf16_grouped_impl(const K3mGemm* gs, int count, hipStream_t st, bool* handled);
+int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st, bool slabs_only);  // gemm_bf16.hip
+int k3m_gemm_bf16_grouped_impl(const K3mGemm* gs, int count, hipStream_t st, bool* handled, const bool* slabs_only);
 
 extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
   if (!gp) return K3M_EINVAL;
-  const K3mGemm& g = *gp;
+  const bool slabs_only = (gp->epilogue & K3M_GEMM_SLABS_ONLY) != 0;
+  K3mGemm gl = *gp;
+  gl.epilogue &= ~K3M_GEMM_SLABS_ONLY;
+  const K3mGemm& g = gl;
+  K3M_ARG(!slabs_only || (g.splitk > 1 && g.ldc == g.n));
   K3M_ARG(g.m >= 0 && g.n >= 0 && g.k >= 0);
   if (g.m == 0 || g.n == 0) return 0;
   K3M_ARG(g.dtype == K3M_F32 || g.dtype == K3M_BF16);
@@ -188,7 +192,7 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
   K3M_ARG(g.epilogue == K3M_EPI_NONE || g.epilogue == K3M_EPI_DGELU || g.bias);
   K3M_ARG((g.epilogue != K3M_EPI_BIAS_GELU && g.epilogue != K3M_EPI_DGELU) || g.aux);
   K3M_ARG(g.f32_algo == K3M_F32_SPLIT_BF16X6 || g.f32_algo == K3M_F32_MFMA_F32);
-  if (g.dtype == K3M_BF16) return k3m_gemm_bf16_impl(g, st);
+  if (g.dtype == K3M_BF16) return k3m_gemm_bf16_impl(g, st, slabs_only);
   // A: K-contiguous iff a_trans == 0; B: K-contiguous iff b_trans == 1
   const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
   const bool av = aligned16(g.a) && (g.lda % 4 == 0) && ((ak ? g.k : g.m) % 4 == 0);
@@ -226,7 +230,7 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
   else rc = launch_tile<64, 64, 2, 2, 2>(g, ak, bk, vec, st);
   if (rc) return rc;
   K3M_CHECK_LAUNCH();
-  if (g.splitk > 1) {
+  if (g.splitk > 1 && !slabs_only) {
     const long long total = (long long)g.m * g.n;
     const int blocks = (int)std::min<long long>((total + 255) / 256, 2048);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, g.ws, g.splitk, g.m, g.n,
@@ -261,18 +265,28 @@ int launch_grouped_epi(const k3m_x6::GemmGroup& grp, int epi, hipStream_t st) {
 
 }  // namespace
 
-extern "C" int k3m_gemm_grouped(const K3mGemm* gs, int count, hipStream_t st) {
-  K3M_ARG(gs && count >= 0 && count <= k3m_x6::GROUP_MAX);
+extern "C" int k3m_gemm_grouped(const K3mGemm* gs_in, int count, hipStream_t st) {
+  K3M_ARG(gs_in && count >= 0 && count <= k3m_x6::GROUP_MAX);
   if (count == 0) return 0;
+  // K3M_GEMM_SLABS_ONLY per problem: stripped here, remembered for the split-K reductions below
+  K3mGemm gs[k3m_x6::GROUP_MAX];
+  bool slabs_only[k3m_x6::GROUP_MAX];
+  for (int i = 0; i < count; ++i) {
+    gs[i] = gs_in[i];
+    slabs_only[i] = (gs[i].epilogue & K3M_GEMM_SLABS_ONLY) != 0;
+    gs[i].epilogue &= ~K3M_GEMM_SLABS_ONLY;
+    K3M_ARG(!slabs_only[i] || (gs[i].splitk > 1 && gs[i].ldc == gs[i].n));
+  }
   // one template for the whole group: same layout, epilogue, dtype, algorithm, 16-B aligned operands
   const K3mGemm& g0 = gs[0];
   if (g0.dtype == K3M_BF16) {   // bf16 encoder: the large-tile grouped kernel (gemm_bf16.hip) when eligible
     bool handled = false;
-    const int r = k3m_gemm_bf16_grouped_impl(gs, count, st, &handled);
+    const int r = k3m_gemm_bf16_grouped_impl(gs, count, st, &handled, slabs_only);
     if (handled || r) return r;
   }
   bool same = g0.dtype == K3M_F32 && g0.c_dtype == K3M_F32 && g0.f32_algo == K3M_F32_SPLIT_BF16X6;
   k3m_x6::GemmGroup grp = {};
+  bool live_slabs[k3m_x6::GROUP_MAX] = {};
   int nb = 0, live = 0;
   long long nb128 = 0, nb256 = 0;
   for (int i = 0; i < count && same; ++i) {
@@ -283,6 +297,7 @@ extern "C" int k3m_gemm_grouped(const K3mGemm* gs, int count, hipStream_t st) {
     same = same && aligned16(g.a) && (g.lda % 4 == 0) && ((ak ? g.k : g.m) % 4 == 0) && aligned16(g.b) &&
            (g.ldb % 4 == 0) && ((bk ? g.k : g.n) % 4 == 0);
     if (g.m == 0 || g.n == 0) continue;
+    live_slabs[live] = slabs_only[i];
     grp.g[live] = g;
     nb128 += nblocks(g, 256, 128);
     nb256 += nblocks(g, 256, 256);
@@ -290,7 +305,9 @@ extern "C" int k3m_gemm_grouped(const K3mGemm* gs, int count, hipStream_t st) {
   }
   if (!same) {   // not one template: launch each on its own
     for (int i = 0; i < count; ++i) {
-      const int rc = k3m_gemm(&gs[i], st);
+      K3mGemm gi = gs[i];
+      if (slabs_only[i]) gi.epilogue |= K3M_GEMM_SLABS_ONLY;
+      const int rc = k3m_gemm(&gi, st);
       if (rc) return rc;
     }
     return 0;
@@ -328,7 +345,7 @@ extern "C" int k3m_gemm_grouped(const K3mGemm* gs, int count, hipStream_t st) {
   K3M_CHECK_LAUNCH();
   for (int i = 0; i < live; ++i) {
     const K3mGemm& g = grp.g[i];
-    if (g.splitk > 1) {
+    if (g.splitk > 1 && !live_slabs[i]) {
       const long long total = (long long)g.m * g.n;
       const int blocks = (int)std::min<long long>((total + 255) / 256, 2048);
       hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, g.ws, g.splitk, g.m, g.n,

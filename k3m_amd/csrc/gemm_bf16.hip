@@ -574,7 +574,7 @@ const bool kBig = [] {
 }  // namespace
 
 // Called by k3m_gemm (gemm.hip) for dtype == K3M_BF16; arguments already validated there.
-int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st) {
+int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st, bool slabs_only) {
   K3M_ARG(g.splitk <= 1 || g.c_dtype == K3M_F32);
   const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
   const bool vec = vec_of(g);
@@ -587,16 +587,18 @@ int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st) {
   }
   if (rc) return rc;
   K3M_CHECK_LAUNCH();
-  return reduce_splits(g, st);
+  return slabs_only ? 0 : reduce_splits(g, st);   // K3M_GEMM_SLABS_ONLY: the caller reduces the slabs
 }
 
 // Grouped bf16 problems (co-attention stages of the bf16 encoder): one large-tile grid when every
 // problem is eligible and shares the template (*handled = true), else nothing is launched.
-int k3m_gemm_bf16_grouped_impl(const K3mGemm* gs, int count, hipStream_t st, bool* handled) {
+int k3m_gemm_bf16_grouped_impl(const K3mGemm* gs, int count, hipStream_t st, bool* handled,
+                               const bool* slabs_only) {
   *handled = false;
   if (!kBig || count <= 0 || count > k3m_b16::GROUP_MAX) return 0;
   const K3mGemm& g0 = gs[0];
   k3m_b16::GemmGroup grp = {};
+  bool live_slabs[k3m_b16::GROUP_MAX] = {};
   int live = 0;
   long long nb256 = 0, nb128 = 0;
   for (int i = 0; i < count; ++i) {
@@ -605,6 +607,7 @@ int k3m_gemm_bf16_grouped_impl(const K3mGemm* gs, int count, hipStream_t st, boo
         g.c_dtype != g0.c_dtype || !big_ok(g, vec_of(g)) || (g.splitk > 1 && g.c_dtype != K3M_F32))
       return 0;
     if (g.m == 0 || g.n == 0) continue;
+    live_slabs[live] = slabs_only[i];
     grp.g[live++] = g;
     nb256 += nb_of(g, 256, 256);
     nb128 += nb_of(g, 256, 128);
@@ -623,6 +626,7 @@ int k3m_gemm_bf16_grouped_impl(const K3mGemm* gs, int count, hipStream_t st, boo
   if (rc) return rc;
   K3M_CHECK_LAUNCH();
   for (int i = 0; i < live; ++i) {
+    if (live_slabs[i]) continue;
     const int r = reduce_splits(grp.g[i], st);
     if (r) return r;
   }

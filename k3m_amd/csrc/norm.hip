@@ -116,15 +116,30 @@ struct SlabJobs {
   int nslab[SLAB_JOBS];
   int cols[SLAB_JOBS];
   int accumulate[SLAB_JOBS];
+  int vec[SLAB_JOBS];         // 1: few slabs, many columns (split-K slabs): 1,024 columns per workgroup
+  int start[SLAB_JOBS + 1];   // first workgroup of each job: a 1-D grid with no idle workgroups when the
+  int njobs;                  // jobs' widths differ (768 .. m*n of a split-K GEMM)
 };
+constexpr int SLAB_VEC_MAX = 64;   // vec mode: nslab <= this, cols % 4 == 0, 16-B aligned
 
 __global__ __launch_bounds__(256) void slab_batch_kernel(SlabJobs jobs) {
   __shared__ float red[4][64];
-  const int j = blockIdx.y;
+  int j = 0;
+  while (j + 1 < jobs.njobs && (int)blockIdx.x >= jobs.start[j + 1]) ++j;   // wave-uniform
   const int cols = jobs.cols[j], nslab = jobs.nslab[j];
+  if (jobs.vec[j]) {
+    // each thread: 4 consecutive columns (16-B loads), every slab in order 0..nslab-1
+    const int c4 = (((int)blockIdx.x - jobs.start[j]) * 256 + (int)threadIdx.x) * 4;
+    if (c4 >= cols) return;
+    const float* src = jobs.ws[j] + c4;
+    floatx4 acc = *reinterpret_cast<const floatx4*>(src);
+    for (int k = 1; k < nslab; ++k) acc += *reinterpret_cast<const floatx4*>(src + (long long)k * cols);
+    floatx4* o = reinterpret_cast<floatx4*>(jobs.out[j] + c4);
+    *o = jobs.accumulate[j] ? *o + acc : acc;
+    return;
+  }
   const int cx = threadIdx.x & 63, ph = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cx;
-  if (blockIdx.x * 64 >= cols) return;   // uniform per workgroup
+  const int c = ((int)blockIdx.x - jobs.start[j]) * 64 + cx;
   const float* src = jobs.ws[j] + min(c, cols - 1);
   float s = 0.f;
   int k = ph;
@@ -493,7 +508,7 @@ extern "C" int k3m_slab_reduce_batch(const float* const* ws, float* const* out, 
     // one launch: consecutive jobs with pairwise different outputs (a repeated output starts the
     // next launch, so accumulations into one array keep their order)
     SlabJobs jb;
-    int n = 0, maxc = 0;
+    int n = 0, nblk = 0;
     for (; j < njobs && n < SLAB_JOBS; ++j) {
       K3M_ARG(ws[j] && out[j] && nslab[j] > 0 && cols[j] > 0);
       bool dup = false;
@@ -504,10 +519,15 @@ extern "C" int k3m_slab_reduce_batch(const float* const* ws, float* const* out, 
       jb.nslab[n] = nslab[j];
       jb.cols[n] = cols[j];
       jb.accumulate[n] = accumulate[j];
-      maxc = std::max(maxc, cols[j]);
+      jb.vec[n] = nslab[j] <= SLAB_VEC_MAX && cols[j] % 4 == 0 && ((uintptr_t)ws[j] & 15) == 0 &&
+                  ((uintptr_t)out[j] & 15) == 0;
+      jb.start[n] = nblk;
+      nblk += jb.vec[n] ? k3m_cdiv(cols[j], 1024) : k3m_cdiv(cols[j], 64);
       ++n;
     }
-    hipLaunchKernelGGL(slab_batch_kernel, dim3(k3m_cdiv(maxc, 64), n), dim3(256), 0, st, jb);
+    jb.start[n] = nblk;
+    jb.njobs = n;
+    hipLaunchKernelGGL(slab_batch_kernel, dim3(nblk), dim3(256), 0, st, jb);
     K3M_CHECK_LAUNCH();
   }
   return 0;

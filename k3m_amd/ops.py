@@ -214,7 +214,13 @@ def linear_wgrad(dy, x, gW, gb=None, alpha=1.0):
     K = x.shape[1]
     s = _splitk(N, K, M, dy.dtype)
     ws = torch.empty((s * N * K,), dtype=torch.float32, device=dy.device) if s > 1 else None
-    gemm(dy, 1, x, 0, gW, N, K, M, L.EPI_NONE, None, None, alpha, 1.0, s, ws)
+    epi = L.EPI_NONE
+    if s > 1 and DEFER and _deferred is not None and alpha == 1.0 and gW.is_contiguous() and _deferred.active_here():
+        # split-K slabs reduced with the block's other slab jobs (K3M_GEMM_SLABS_ONLY): gW += sum of slabs
+        epi |= L.GEMM_SLABS_ONLY
+        _deferred.keep.append(ws)
+        _deferred.add(ptr(ws), gW, s, N * K)
+    gemm(dy, 1, x, 0, gW, N, K, M, epi, None, None, alpha, 1.0, s, ws)
     if gb is not None:
         if _grouper is not None:   # dy may come from a side-stream branch of the same grouped block
             _grouper.after.append(lambda: colsum(dy, gb, accumulate=True, alpha=alpha))
