@@ -54,47 +54,63 @@ def heads(x, nh):
     return x.view(B, L, nh, D // nh).permute(0, 2, 1, 3)
 
 
-def attend(q, k, v, mask_add, nh):
-    """softmax(q k^T / sqrt(d) + mask) v, heads split from the last dim (vilbert_k3m.py:439-475)."""
+def _drop(x, drop, site):
+    """Training-mode dropout with an explicit mask (0 or 1/(1-p) per element) — the oracle is fed the
+    masks of the implementation under test (tests/test_gpu_train_mode_parity.py); eval mode (None)
+    is the identity, as nn.Dropout in model.eval()."""
+    if drop is None or drop.get(site) is None:
+        return x
+    return x * drop[site].to(x.dtype).reshape(x.shape)
+
+
+def attend(q, k, v, mask_add, nh, drop=None, site="attn"):
+    """softmax(q k^T / sqrt(d) + mask) v, heads split from the last dim (vilbert_k3m.py:439-475);
+    dropout on the probabilities (:466)."""
     d = q.shape[-1] // nh
     qh, kh, vh = heads(q, nh), heads(k, nh), heads(v, nh)
     s = qh @ kh.transpose(-1, -2) / math.sqrt(d) + mask_add
-    p = torch.softmax(s, dim=-1)
+    p = _drop(torch.softmax(s, dim=-1), drop, site)
     ctx = (p @ vh).permute(0, 2, 1, 3).contiguous()
     return ctx.view(ctx.shape[0], ctx.shape[1], -1)
 
 
 # ---------------------------------------------------------------- layers
 
-def bert_layer(P, pre, x, mask_add, nh):
-    """BertLayer / BertImageLayer (vilbert_k3m.py:535-548, :696-709), post-LN."""
+def bert_layer(P, pre, x, mask_add, nh, drop=None):
+    """BertLayer / BertImageLayer (vilbert_k3m.py:535-548, :696-709), post-LN.  ``drop`` (training
+    mode): masks for "attn" (probabilities, :466), "attn_out" (BertSelfOutput :487) and "ffn_out"
+    (BertOutput :530)."""
     q = linear(P, pre + ".attention.self.query", x)
     k = linear(P, pre + ".attention.self.key", x)
     v = linear(P, pre + ".attention.self.value", x)
-    ctx = attend(q, k, v, mask_add, nh)
-    a = layer_norm(linear(P, pre + ".attention.output.dense", ctx) + x,
+    ctx = attend(q, k, v, mask_add, nh, drop, "attn")
+    a = layer_norm(_drop(linear(P, pre + ".attention.output.dense", ctx), drop, "attn_out") + x,
                    P[pre + ".attention.output.LayerNorm.weight"], P[pre + ".attention.output.LayerNorm.bias"])
     f = gelu(linear(P, pre + ".intermediate.dense", a))
-    return layer_norm(linear(P, pre + ".output.dense", f) + a,
+    return layer_norm(_drop(linear(P, pre + ".output.dense", f), drop, "ffn_out") + a,
                       P[pre + ".output.LayerNorm.weight"], P[pre + ".output.LayerNorm.bias"])
 
 
-def connection_layer(P, pre, s1, m1, s2, m2, nh):
+def connection_layer(P, pre, s1, m1, s2, m2, nh, drop=None):
     """BertConnectionLayer(_two_text) (vilbert_k3m.py:1030-1111) with BertBiAttention :753-838
-    and BertBiOutput :986-996.  Stream 1 attends to stream 2 and vice versa."""
+    and BertBiOutput :986-996.  Stream 1 attends to stream 2 and vice versa.  ``drop`` (training
+    mode): "attn1" / "attn2" (probabilities, :797 / :819), "out1" / "out2" (BiOutput :988 / :991),
+    "ffn1" / "ffn2" (v_output / t_output)."""
     b = pre + ".biattention."
     q1, k1, v1 = linear(P, b + "query1", s1), linear(P, b + "key1", s1), linear(P, b + "value1", s1)
     q2, k2, v2 = linear(P, b + "query2", s2), linear(P, b + "key2", s2), linear(P, b + "value2", s2)
-    ctx1 = attend(q2, k1, v1, m1, nh)   # stream-2 queries over stream-1 keys
-    ctx2 = attend(q1, k2, v2, m2, nh)   # stream-1 queries over stream-2 keys
+    ctx1 = attend(q2, k1, v1, m1, nh, drop, "attn1")   # stream-2 queries over stream-1 keys
+    ctx2 = attend(q1, k2, v2, m2, nh, drop, "attn2")   # stream-1 queries over stream-2 keys
     o = pre + ".biOutput."
-    h1 = layer_norm(linear(P, o + "dense1", ctx2) + s1, P[o + "LayerNorm1.weight"], P[o + "LayerNorm1.bias"])
-    h2 = layer_norm(linear(P, o + "dense2", ctx1) + s2, P[o + "LayerNorm2.weight"], P[o + "LayerNorm2.bias"])
+    h1 = layer_norm(_drop(linear(P, o + "dense1", ctx2), drop, "out1") + s1, P[o + "LayerNorm1.weight"],
+                    P[o + "LayerNorm1.bias"])
+    h2 = layer_norm(_drop(linear(P, o + "dense2", ctx1), drop, "out2") + s2, P[o + "LayerNorm2.weight"],
+                    P[o + "LayerNorm2.bias"])
     f1 = gelu(linear(P, pre + ".v_intermediate.dense", h1))
-    y1 = layer_norm(linear(P, pre + ".v_output.dense", f1) + h1,
+    y1 = layer_norm(_drop(linear(P, pre + ".v_output.dense", f1), drop, "ffn1") + h1,
                     P[pre + ".v_output.LayerNorm.weight"], P[pre + ".v_output.LayerNorm.bias"])
     f2 = gelu(linear(P, pre + ".t_intermediate.dense", h2))
-    y2 = layer_norm(linear(P, pre + ".t_output.dense", f2) + h2,
+    y2 = layer_norm(_drop(linear(P, pre + ".t_output.dense", f2), drop, "ffn2") + h2,
                     P[pre + ".t_output.LayerNorm.weight"], P[pre + ".t_output.LayerNorm.bias"])
     return y1, y2
 
