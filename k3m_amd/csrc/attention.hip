@@ -987,10 +987,7 @@ void launch_bwd(const void* dctx, long long ldc, const void* o, long long ldo, c
 }  // namespace
 
 // the register-softmax forward serves fp32 heads whose K and V fit 2 workgroups per CU
-static const bool kAttnFwdReg = [] {
-  const char* e = std::getenv("K3M_ATTN_FWD_REG");
-  return !(e && e[0] == '0');
-}();
+static const bool kAttnFwdReg = k3m_env_flag("K3M_ATTN_FWD_REG", true);
 
 template <int HD>
 void launch_fwd_reg(const void* q, long long ldq, const void* k, long long ldk, const void* v, long long ldv,
@@ -1038,10 +1035,7 @@ extern "C" int k3m_attn_fwd(const void* q, long long ldq, const void* k, long lo
   return 0;
 }
 
-static const bool kAttnBwdReg = [] {
-  const char* e = std::getenv("K3M_ATTN_BWD_REG");
-  return !(e && e[0] == '0');
-}();
+static const bool kAttnBwdReg = k3m_env_flag("K3M_ATTN_BWD_REG", true);
 
 template <int HD>
 void launch_bwd_reg(const void* dctx, long long ldc, const void* o, long long ldo, const void* q, long long ldq,

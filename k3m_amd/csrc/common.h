@@ -169,3 +169,16 @@ __device__ __forceinline__ float dgelu_fast(float x) {
 }
 
 static inline int k3m_cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// Environment knobs (A/B switches), read once at library load.  Plain functions, not lambda
+// initialisers: hipcc (ROCm 7.2) gives the closures of lambdas in REOPENED anonymous namespaces the
+// same mangled name ($_0 ...), so one knob's initialiser silently ran another's getenv.
+#include <cstdlib>
+static inline int k3m_env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+static inline bool k3m_env_flag(const char* name, bool dflt) {   // "0" = off, anything else = on
+  const char* e = std::getenv(name);
+  return e ? !(e[0] == '0') : dflt;
+}

@@ -120,10 +120,7 @@ long long nblocks(const K3mGemm& g, int bm, int bn) {
 // of 256 blocks (the 8,192-row co-attention FFN: 384 blocks = 1.5 waves vs 768 = 3).
 // K3M_X6_TILE256 (bitmask, default 15): 1 forward (both K-contiguous), 2 dgrad (B MN-contiguous),
 // 4 weight gradients (both MN-contiguous), 8 the grouped launch; 0 keeps every GEMM on 256x128.
-const int kTile256 = [] {
-  const char* e = std::getenv("K3M_X6_TILE256");
-  return e ? std::atoi(e) : 15;
-}();
+const int kTile256 = k3m_env_int("K3M_X6_TILE256", 15);
 
 int tile256_class(bool ak, bool bk) { return ak && bk ? 1 : ak ? 2 : !bk ? 4 : 0; }
 
@@ -135,10 +132,7 @@ bool prefer_256x256(const K3mGemm& g) {
 
 // Persistent x6 walk (gemm_x6p.hip) for the 256-row tiles: K3M_X6_PERSIST=0 restores one workgroup per
 // tile (A/B knob).
-const int kPersist = [] {
-  const char* e = std::getenv("K3M_X6_PERSIST");
-  return e ? std::atoi(e) : 1;
-}();
+const int kPersist = k3m_env_int("K3M_X6_PERSIST", 1);
 
 int cu_count() {
   static int n = [] {
@@ -155,10 +149,7 @@ int cu_count() {
 int k3m_x6_persistent_launch(const k3m_x6::GemmGroup& grp, bool t256, bool ak, bool bk, int cus, hipStream_t st);
 int k3m_x6_variant_launch(const K3mGemm& g, int variant, hipStream_t st);   // lab tiles (gemm_x6p.hip)
 namespace {
-const int kVariant = [] {
-  const char* e = std::getenv("K3M_X6_VARIANT");
-  return e ? std::atoi(e) : 0;
-}();
+const int kVariant = k3m_env_int("K3M_X6_VARIANT", 0);
 }  // namespace
 
 namespace {

@@ -454,10 +454,7 @@ long long nb_of(const K3mGemm& g, int bm, int bn) {
 // MFMA shape per operand layout: 16x16x32 when B is K-contiguous (forward), 32x32x16 when it is
 // MN-contiguous (input and weight gradients: their transposing fragment reads fit the LDS counter
 // per 16-deep substep); K3M_B16_MF=16 / 32 forces one shape everywhere (A/B).
-const int kMF = [] {
-  const char* e = std::getenv("K3M_B16_MF");
-  return e ? std::atoi(e) : 0;
-}();
+const int kMF = k3m_env_int("K3M_B16_MF", 0);
 inline bool use_mf32(bool bk) { return kMF == 32 || (kMF != 16 && !bk); }
 
 template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, typename CT, int MF>
@@ -566,10 +563,7 @@ bool vec_of(const K3mGemm& g) {
 }
 
 // K3M_BF16_BIG=0 keeps every bf16 GEMM on the 128x128 register-staged kernel (A/B switch)
-const bool kBig = [] {
-  const char* e = std::getenv("K3M_BF16_BIG");
-  return !(e && e[0] == '0');
-}();
+const bool kBig = k3m_env_flag("K3M_BF16_BIG", true);
 
 }  // namespace
 

@@ -276,7 +276,34 @@ int k3m_x6_persistent_launch(const k3m_x6::GemmGroup& grp, bool t256, bool ak, b
 // order for loads AND stores, so inside one workgroup a tile's stores stall the next tile's loads).
 int k3m_x6_variant_launch(const K3mGemm& g, int variant, hipStream_t st) {
   const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
-  if ((variant != 1 && variant != 2) || !(ak && bk)) return -1;
+  if (variant < 1 || variant > 4 || !(ak && bk) || (variant >= 3 && g.epilogue == K3M_EPI_DGELU)) return -1;
+  if (variant >= 3 && g.epilogue != K3M_EPI_DGELU) {
+    // one wave per SIMD: 256x256 tile over 2x2 waves of 128x128 (256 accumulators, up to 512 registers
+    // per wave): twice the MFMAs per fragment read, no register aliasing between the staged global loads
+    // and the fragments (variant 3: two register sets, 4: one)
+    const int tm3 = (g.m + 255) / 256, tn3 = (g.n + 255) / 256;
+    dim3 grid3(tm3 * tn3, g.splitk > 1 ? g.splitk : 1);
+    switch (g.epilogue) {
+#define K3M_V3_CASE(E)                                                                                     \
+      case E:                                                                                              \
+        if (variant == 3)                                                                                  \
+          hipLaunchKernelGGL((k3m_x6::gemm_x6_kernel<256, 256, 2, 2, 16, true, true, true, E, 1, true>), grid3, \
+                             dim3(256), 0, st, g);                                                         \
+        else                                                                                               \
+          hipLaunchKernelGGL((k3m_x6::gemm_x6_kernel<256, 256, 2, 2, 16, true, true, true, E, 1, false>), grid3, \
+                             dim3(256), 0, st, g);                                                         \
+        break;
+      K3M_V3_CASE(K3M_EPI_NONE)
+      K3M_V3_CASE(K3M_EPI_BIAS)
+      K3M_V3_CASE(K3M_EPI_BIAS_GELU)
+      K3M_V3_CASE(K3M_EPI_DGELU)
+      K3M_V3_CASE(K3M_EPI_BIAS_SIGMOID)
+#undef K3M_V3_CASE
+      default: return K3M_EINVAL;
+    }
+    K3M_CHECK_LAUNCH();
+    return 0;
+  }
   const int tm = (g.m + 127) / 128, tn = (g.n + 255) / 256;
   dim3 grid(tm * tn, g.splitk > 1 ? g.splitk : 1);
   switch (g.epilogue) {
