@@ -311,8 +311,11 @@ def main():
     barrier()
     probe.active = cprobe.active = True
     t0 = time.perf_counter()
+    host = 0.0
     for _ in range(args.steps):
+        h0 = time.perf_counter()
         out = tr.step(batch)
+        host += time.perf_counter() - h0
     barrier()
     dt = time.perf_counter() - t0
     probe.active = cprobe.active = False
@@ -352,6 +355,9 @@ def main():
                    "model": "bert_base_6layer_6conect", "global_batch": B * world, "seq_len": T,
                    "parallelism": "dp%d" % world},
         "per_gpu_samples_s": round(value / world, 3),
+        # host time to issue one step (Python engine + launches; the GPU runs behind it): when this
+        # approaches ms_per_step the step is launch-bound and the GPU idles between kernels
+        "host_ms_per_step": round(1000.0 * host / args.steps, 3),
         "loss": round(loss, 4),
         "step_mfma_frac_vs_ref_flops": round(B * ref_sample / (ms_step * 1e-3) / peak, 4),
         "roofline": {"bound": "mfma", "kernel": "%s text-layer FFN1 %dx%dx%d" % (kname, Mg, Ng, Kg),

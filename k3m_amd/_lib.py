@@ -11,7 +11,8 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libk3m_hip.so")
+# K3M_LIB: another build of the same library (same-box A/B of two builds, scripts/ab_lib.sh)
+LIB_PATH = os.environ.get("K3M_LIB") or os.path.join(_HERE, "libk3m_hip.so")
 
 F32, BF16 = 0, 1
 EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_DGELU, EPI_BIAS_SIGMOID = 0, 1, 2, 3, 4
@@ -122,11 +123,27 @@ def ptr(t):
     return None if t is None else t.data_ptr()
 
 
+try:   # the raw current-stream handle without building a torch.cuda.Stream (1,400 launches per step)
+    _raw_stream = torch._C._cuda_getCurrentRawStream
+    _cur_dev = torch._C._cuda_getDevice
+except AttributeError:   # pragma: no cover - older torch
+    _raw_stream = None
+
+
 def stream():
+    """hipStream_t (as int) of the current stream of the current device."""
+    if _raw_stream is not None:
+        return _raw_stream(_cur_dev())
     return torch.cuda.current_stream().cuda_stream
 
 
+_fns = {}
+
+
 def call(name, *args):
-    rc = getattr(load(), name)(*args)
+    fn = _fns.get(name)
+    if fn is None:
+        fn = _fns[name] = getattr(load(), name)
+    rc = fn(*args)
     if rc != 0:
         raise RuntimeError("%s failed with status %d (%s)" % (name, rc, "bad argument" if rc == 1 else "hip error %d" % -rc))

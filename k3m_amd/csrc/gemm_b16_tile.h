@@ -23,6 +23,8 @@
 #pragma once
 #include "common.h"
 
+#include <type_traits>
+
 namespace k3m_b16 {
 
 constexpr int BK = 64;
@@ -363,12 +365,38 @@ template <> struct Raw8<float> {
   }
 };
 
+template <int EPI>
+__device__ __forceinline__ void epi_math8(const float (&v)[8], const float (&bb)[8], const float (&ax)[8],
+                                          const float (&old)[8], float alpha, float beta, bool rd_old,
+                                          float (&o)[8], float (&pa)[8]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    if constexpr (EPI == K3M_EPI_NONE) {
+      o[e] = alpha * v[e];
+    } else if constexpr (EPI == K3M_EPI_BIAS) {
+      o[e] = alpha * (v[e] + bb[e]);
+    } else if constexpr (EPI == K3M_EPI_BIAS_GELU) {
+      pa[e] = v[e] + bb[e];
+      o[e] = gelu_fast(to_f(from_f<bf16_t>(pa[e])));  // gelu of the stored pre-activation the backward sees
+    } else if constexpr (EPI == K3M_EPI_DGELU) {
+      o[e] = alpha * v[e] * dgelu_fast(ax[e]);
+    } else {
+      o[e] = sigmoid_f(v[e] + bb[e]);
+    }
+    if (rd_old) o[e] = fmaf(beta, old[e], o[e]);
+  }
+}
+
 // Epilogue through LDS (the stages are free after the main loop): per pass each wave stages 32 rows
 // x (TBN/WN) columns of its fp32 accumulators (row stride TBN/WN + 8 floats), then every lane
 // handles 8 consecutive columns of one row: epilogue math, 16-B (bf16) / 32-B (fp32) stores.
-// The C (beta) / aux (dGELU) values it reads are loaded ahead: two 32-row groups in flight for bf16
-// C, one for fp32 C (register budget) — a load issued right before its use exposed a full HBM latency
-// per row group and made the output-heavy epilogues latency-bound.
+// vmcnt counts loads and stores in issue order, so a load issued after a store cannot be waited for
+// without draining that store.  Hence: the lane's 8 bias values (the same columns in every pass) are
+// loaded once with vector loads and waited for before the first store, and interior tiles (inside C,
+// 16-B aligned rows) run a branch-free pass sequence whose per-pass loads (dGELU pre-activation, old C
+// for beta != 0) are issued RING passes ahead — the compiler can then count its waits instead of
+// falling back to vmcnt(0) (which had drained every store of a pass before the next one).  Edge tiles
+// keep the guarded per-element path.
 // 16x16 accumulator layout: acc[i][j][r] = C[wm + 16 i + 4 (lane >> 4) + r][wn + 16 j + (lane & 15)].
 template <int TBM, int TBN, int WM, int WN, int EPI, typename CT, typename AccT>
 __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint16_t* smem_u16, const AccT& acc,
@@ -376,6 +404,7 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint1
   using S = Shape<TBM, TBN, WM, WN>;
   constexpr int WNC = TBN / WN, WS = WNC + 8, LPR = WNC / 8, RPP = 64 / LPR, NPS = 32 / RPP, NG = TBM / WM / 32;
   static_assert(S::NT / 64 * 32 * WS * 4 <= S::LDS * 2, "epilogue staging exceeds the LDS stages");
+  constexpr int RING = sizeof(CT) == 2 ? 2 : 1;   // passes the per-pass loads run ahead (register budget)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = (w / WN) * (TBM / WM), wn = (w % WN) * WNC;
   float* wl = reinterpret_cast<float*>(smem_u16) + w * 32 * WS;
@@ -393,79 +422,94 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint1
                     (!HAS_AUX || ((g.ldaux % 8 == 0) && ((reinterpret_cast<uintptr_t>(aux) & 15) == 0)));
   const int lr = lane / LPR, lc = (lane % LPR) * 8;
   const int col = n0 + wn + lc;
-  float bb[8];
+  float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if constexpr (HAS_BIAS) {
+    if (((reinterpret_cast<uintptr_t>(bias) & 15) == 0) && col + 8 <= N) {
+      load8(bias + col, bb);
+    } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) bb[e] = col + e < N ? bias[col + e] : 0.f;
+      for (int e = 0; e < 8; ++e) bb[e] = col + e < N ? bias[col + e] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) asm volatile("" ::"v"(bb[e]));   // waited for here, before any store
   }
   const bool rd_old = CAN_OLD && beta != 0.f;
-  // prefetch ring: PD row groups of (dGELU aux | old C) values ahead
-  constexpr bool PRE = EPI == K3M_EPI_DGELU || CAN_OLD;
-  constexpr int PD = (sizeof(CT) == 2 && NG >= 2) ? 2 : 1;   // groups in flight (register budget)
-  Raw8<CT> pax[PRE && EPI == K3M_EPI_DGELU ? PD : 1][NPS], pold[PRE ? PD : 1][NPS];
   auto row_of = [&](int grp, int ps) { return m0 + wm + 32 * grp + ps * RPP + lr; };
-  auto prefetch = [&](int grp, int slot) {
-#pragma unroll
-    for (int ps = 0; ps < NPS; ++ps) {
-      const int row = row_of(grp, ps);
-      if (row < M && cvec && col + 8 <= N) {
-        if constexpr (EPI == K3M_EPI_DGELU) pax[slot][ps].load(aux + (long long)row * g.ldaux + col);
-        if constexpr (CAN_OLD) {
-          if (rd_old) pold[slot][ps].load(C + (long long)row * ldc + col);
+  if (cvec && m0 + TBM <= M && n0 + TBN <= N) {
+    auto body = [&](auto old_tag) {
+      constexpr bool OLD = decltype(old_tag)::value;
+      constexpr bool LOADS = OLD || EPI == K3M_EPI_DGELU;
+      constexpr int NQ = NG * NPS;
+      Raw8<CT> rax[EPI == K3M_EPI_DGELU ? RING : 1], rold[OLD ? RING : 1];
+      auto issue = [&](int q, int slot) {
+        if constexpr (LOADS) {
+          const long long r = row_of(q / NPS, q % NPS);
+          if constexpr (EPI == K3M_EPI_DGELU) rax[slot].load(aux + r * g.ldaux + col);
+          if constexpr (OLD) rold[slot].load(C + r * ldc + col);
         }
-      }
-    }
-  };
-  if constexpr (PRE) {
+      };
 #pragma unroll
-    for (int q = 0; q < PD; ++q) prefetch(q, q);
+      for (int q = 0; q < RING; ++q)
+        if (q < NQ) issue(q, q);
+#pragma unroll
+      for (int grp = 0; grp < NG; ++grp) {
+        acc.stage(grp, wl, WS, lane);
+        __syncthreads();
+#pragma unroll
+        for (int ps = 0; ps < NPS; ++ps) {
+          const int q = grp * NPS + ps, slot = q % RING;
+          const int rr = ps * RPP + lr;
+          const long long row = row_of(grp, ps);
+          const floatx4 v0 = *reinterpret_cast<const floatx4*>(wl + rr * WS + lc);
+          const floatx4 v1 = *reinterpret_cast<const floatx4*>(wl + rr * WS + lc + 4);
+          const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+          float ax[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, old[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          if constexpr (EPI == K3M_EPI_DGELU) rax[slot].get(ax);
+          if constexpr (OLD) rold[slot].get(old);
+          if (q + RING < NQ) issue(q + RING, slot);
+          float o[8], pa[8];
+          epi_math8<EPI>(v, bb, ax, old, alpha, beta, OLD, o, pa);
+          store8(C + row * ldc + col, o);
+          if constexpr (EPI == K3M_EPI_BIAS_GELU) store8(aux + row * g.ldaux + col, pa);
+        }
+        __syncthreads();
+      }
+    };
+    if (rd_old) body(std::integral_constant<bool, true>());
+    else body(std::integral_constant<bool, false>());
+    return;
   }
+  // edge tiles: guarded per-element accesses (rolled pass loop: small code, few registers)
 #pragma unroll
   for (int grp = 0; grp < NG; ++grp) {
-    const int slot = grp % PD;
     acc.stage(grp, wl, WS, lane);
     __syncthreads();
-#pragma unroll
+#pragma unroll 1
     for (int ps = 0; ps < NPS; ++ps) {
       const int rr = ps * RPP + lr;
       const int row = row_of(grp, ps);
       const floatx4 v0 = *reinterpret_cast<const floatx4*>(wl + rr * WS + lc);
       const floatx4 v1 = *reinterpret_cast<const floatx4*>(wl + rr * WS + lc + 4);
       if (row >= M || col >= N) continue;
-      float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
       const bool full = cvec && col + 8 <= N;
       CT* cp = C + (long long)row * ldc + col;
       CT* ap = HAS_AUX ? aux + (long long)row * g.ldaux + col : nullptr;
-      float old[8], ax[8];
+      float old[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ax[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if constexpr (EPI == K3M_EPI_DGELU) {
-        if (full) pax[slot][ps].get(ax);
+        if (full) load8(ap, ax);
         else
 #pragma unroll
           for (int e = 0; e < 8; ++e) ax[e] = col + e < N ? to_f(ap[e]) : 0.f;
       }
       if (rd_old) {
-        if (full) pold[slot][ps].get(old);
+        if (full) load8(cp, old);
         else
 #pragma unroll
           for (int e = 0; e < 8; ++e) old[e] = col + e < N ? to_f(cp[e]) : 0.f;
       }
       float o[8], pa[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        if constexpr (EPI == K3M_EPI_NONE) {
-          o[e] = alpha * v[e];
-        } else if constexpr (EPI == K3M_EPI_BIAS) {
-          o[e] = alpha * (v[e] + bb[e]);
-        } else if constexpr (EPI == K3M_EPI_BIAS_GELU) {
-          pa[e] = v[e] + bb[e];
-          o[e] = gelu_fast(to_f(from_f<CT>(pa[e])));  // gelu of the stored pre-activation the backward sees
-        } else if constexpr (EPI == K3M_EPI_DGELU) {
-          o[e] = alpha * v[e] * dgelu_fast(ax[e]);
-        } else {
-          o[e] = sigmoid_f(v[e] + bb[e]);
-        }
-        if (rd_old) o[e] = fmaf(beta, old[e], o[e]);
-      }
+      epi_math8<EPI>(v, bb, ax, old, alpha, beta, rd_old, o, pa);
       if (full) {
         store8(cp, o);
         if constexpr (EPI == K3M_EPI_BIAS_GELU) store8(ap, pa);
@@ -477,9 +521,6 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint1
             if constexpr (EPI == K3M_EPI_BIAS_GELU) ap[e] = from_f<CT>(pa[e]);
           }
       }
-    }
-    if constexpr (PRE) {
-      if (grp + PD < NG) prefetch(grp + PD, slot);   // refill the slot just consumed
     }
     __syncthreads();
   }

@@ -20,6 +20,12 @@
 #pragma once
 #include "common.h"
 
+#include <type_traits>
+
+#ifndef K3M_EPI_RING
+#define K3M_EPI_RING 1
+#endif
+
 // The lab (scripts/lab) compiles these templates into its own executable under other namespace
 // names: kernels with the same mangled name as libk3m_hip.so's would resolve to the library's code.
 #ifndef K3M_F32_NS
@@ -215,16 +221,67 @@ struct NoHook {
 // hook(): called once, after the first accumulator slice is in LDS and before any global store (the
 // persistent x6 kernel issues the next tile's loads there, when acc[0] is dead and the loads are
 // older than every store of this tile).
-template <int TBM, int TBN, int WM, int WN, int EPI, int CAP = 2 * (TBM + TBN) * BK, class Hook = NoHook>
-__device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, float* smem,
-                                         const floatx16 (&acc)[TBM / WM / 32][TBN / WN / 32], int slice = -1,
-                                         Hook hook = Hook()) {
+// The epilogue reads the accumulators through a stager: stage(i, wl, ws, lane) writes the wave's
+// 32-row group i into its [32][ws] fp32 LDS region (row-major, column 0 = the wave's first column).
+template <int FM, int FN>
+struct Acc32Ref {   // v_mfma_f32_32x32x*: acc[i][j][r] = row (r&3) + 8*(r>>2) + 4*(lane>>5), col lane&31
+  const floatx16 (&a)[FM][FN];
+  __device__ __forceinline__ void stage(int i, float* wl, int ws, int lane) const {
+    const int kl = lane >> 5, cl = lane & 31;
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) wl[((r & 3) + 8 * (r >> 2) + 4 * kl) * ws + 32 * j + cl] = a[i][j][r];
+  }
+};
+
+__device__ __forceinline__ void ld8(const float* p, float (&v)[8]) {
+  const floatx4 a = *reinterpret_cast<const floatx4*>(p), b = *reinterpret_cast<const floatx4*>(p + 4);
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+__device__ __forceinline__ void st8(float* p, const float (&v)[8]) {
+  *reinterpret_cast<floatx4*>(p) = floatx4{v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<floatx4*>(p + 4) = floatx4{v[4], v[5], v[6], v[7]};
+}
+
+template <int EPI>
+__device__ __forceinline__ void epi_math(const float (&v)[8], const float (&bb)[8], const float (&ax)[8],
+                                         const float (&old)[8], float alpha, float beta, bool rd_old, float (&o)[8],
+                                         float (&pa)[8]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    if constexpr (EPI == K3M_EPI_NONE) {
+      o[e] = alpha * v[e];
+    } else if constexpr (EPI == K3M_EPI_BIAS) {
+      o[e] = alpha * (v[e] + bb[e]);
+    } else if constexpr (EPI == K3M_EPI_BIAS_GELU) {
+      pa[e] = v[e] + bb[e];
+      o[e] = gelu_f(pa[e]);
+    } else if constexpr (EPI == K3M_EPI_DGELU) {
+      o[e] = alpha * v[e] * dgelu_f(ax[e]);
+    } else {
+      o[e] = sigmoid_f(v[e] + bb[e]);
+    }
+    if (rd_old) o[e] += beta * old[e];
+  }
+}
+
+// Global traffic of the epilogue is kept out of its own way.  vmcnt counts loads AND stores in issue
+// order, so a load issued after a store cannot be waited for without waiting for that store: a
+// per-pass bias load drained every store of the previous pass before the next pass could compute
+// (one `s_waitcnt vmcnt(0)` per pass in the ISA, profiles/r3_epilogue_vmcnt.txt).  So (1) the lane's
+// 8 bias values (its columns are the same in every pass) are loaded once and waited for before the
+// first store; (2) interior tiles (inside C, 16-B aligned rows) run a branch-free pass sequence whose
+// per-pass loads (dGELU pre-activation, old C for beta != 0) are issued RING passes ahead, so waiting
+// for them retires only the stores of passes RING or more back.
+template <int TBM, int TBN, int WM, int WN, int EPI, int CAP, class Hook, class AccR, bool FAST = true>
+__device__ __forceinline__ void epilogue_r(const K3mGemm& g, int m0, int n0, float* smem, const AccR& acc, int slice,
+                                           Hook hook) {
   constexpr int FM = TBM / WM / 32, FN = TBN / WN / 32;
-  constexpr int WCOLS = FN * 32, WS = WCOLS + 8, LPR = WCOLS / 8, RPP = 64 / LPR;
+  constexpr int WCOLS = FN * 32, WS = WCOLS + 8, LPR = WCOLS / 8, RPP = 64 / LPR, NPS = 32 / RPP;
   static_assert(WM * WN * 32 * WS <= CAP, "epilogue staging exceeds the LDS tile");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = (w / WN) * (TBM / WM), wn = (w % WN) * (TBN / WN);
-  const int kl = lane >> 5, cl = lane & 31;
   const int M = g.m, N = g.n;
   float* wl = smem + w * 32 * WS;
   const bool split = g.splitk > 1;
@@ -235,24 +292,85 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, float
   const float* bias = g.bias;
   constexpr bool HAS_AUX = EPI == K3M_EPI_BIAS_GELU || EPI == K3M_EPI_DGELU;
   constexpr bool HAS_BIAS = EPI == K3M_EPI_BIAS || EPI == K3M_EPI_BIAS_GELU || EPI == K3M_EPI_BIAS_SIGMOID;
+  constexpr bool CAN_OLD = EPI == K3M_EPI_NONE || EPI == K3M_EPI_BIAS || EPI == K3M_EPI_DGELU;
   const bool cvec = (ldc % 4 == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) &&
                     (!HAS_AUX || ((g.ldaux % 4 == 0) && ((reinterpret_cast<uintptr_t>(aux) & 15) == 0)));
-  const bool rd_old = (EPI == K3M_EPI_NONE || EPI == K3M_EPI_BIAS || EPI == K3M_EPI_DGELU) && beta != 0.f;
+  const bool rd_old = CAN_OLD && beta != 0.f;
   const bool bvec = HAS_BIAS && ((reinterpret_cast<uintptr_t>(bias) & 15) == 0);
   const int lr = lane / LPR, lc = (lane % LPR) * 8;
+  const int col = n0 + wn + lc;
+  float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if constexpr (HAS_BIAS) {
+    if (bvec && col + 8 <= N) {
+      ld8(bias + col, bb);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bb[e] = col + e < N ? bias[col + e] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) asm volatile("" ::"v"(bb[e]));   // waited for here, before any store
+  }
+  auto row_of = [&](int i, int ps) { return m0 + wm + 32 * i + ps * RPP + lr; };
+  // passes the per-pass loads run ahead (their registers: RING x 8 floats per load stream)
+  constexpr int RING = K3M_EPI_RING;
+  const bool interior = FAST && cvec && m0 + TBM <= M && n0 + TBN <= N;
+  if constexpr (FAST) if (interior) {
+    auto body = [&](auto old_tag) {
+      constexpr bool OLD = decltype(old_tag)::value;
+      constexpr bool LOADS = OLD || EPI == K3M_EPI_DGELU;
+      constexpr int NQ = FM * NPS;
+      float rax[RING][8], rold[RING][8];
+      auto issue = [&](int q, int slot) {
+        if constexpr (LOADS) {
+          const long long r = row_of(q / NPS, q % NPS);
+          if constexpr (EPI == K3M_EPI_DGELU) ld8(aux + r * g.ldaux + col, rax[slot]);
+          if constexpr (OLD) ld8(C + r * ldc + col, rold[slot]);
+        }
+      };
+#pragma unroll
+      for (int q = 0; q < RING; ++q)
+        if (q < NQ) issue(q, q);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        acc.stage(i, wl, WS, lane);
+        __syncthreads();
+        if (i == 0) hook();
+#pragma unroll
+        for (int ps = 0; ps < NPS; ++ps) {
+          const int q = i * NPS + ps, slot = q % RING;
+          const int rr = ps * RPP + lr;
+          const long long row = row_of(i, ps);
+          const floatx4 v0 = *reinterpret_cast<const floatx4*>(wl + rr * WS + lc);
+          const floatx4 v1 = *reinterpret_cast<const floatx4*>(wl + rr * WS + lc + 4);
+          const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+          float ax[8], old[8], o[8], pa[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            ax[e] = LOADS && EPI == K3M_EPI_DGELU ? rax[slot][e] : 0.f;
+            old[e] = OLD ? rold[slot][e] : 0.f;
+          }
+          if (q + RING < NQ) issue(q + RING, slot);
+          epi_math<EPI>(v, bb, ax, old, alpha, beta, OLD, o, pa);
+          st8(C + row * ldc + col, o);
+          if constexpr (EPI == K3M_EPI_BIAS_GELU) st8(aux + row * g.ldaux + col, pa);
+        }
+        __syncthreads();
+      }
+    };
+    if (rd_old) body(std::integral_constant<bool, true>());
+    else body(std::integral_constant<bool, false>());
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) wl[((r & 3) + 8 * (r >> 2) + 4 * kl) * WS + 32 * j + cl] = acc[i][j][r];
+    acc.stage(i, wl, WS, lane);
     __syncthreads();
     if (i == 0) hook();
-#pragma unroll
-    for (int ps = 0; ps < 32 / RPP; ++ps) {
+    // edge tiles only: a rolled pass loop keeps this path's code (and its registers) small
+#pragma unroll 1
+    for (int ps = 0; ps < NPS; ++ps) {
       const int rr = ps * RPP + lr;
-      const int row = m0 + wm + 32 * i + rr;
-      const int col = n0 + wn + lc;
+      const int row = row_of(i, ps);
       const floatx4 v0 = *reinterpret_cast<const floatx4*>(wl + rr * WS + lc);
       const floatx4 v1 = *reinterpret_cast<const floatx4*>(wl + rr * WS + lc + 4);
       if (row >= M || col >= N) continue;
@@ -260,58 +378,24 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, float
       const bool full = cvec && col + 8 <= N;
       float* cp = C + (long long)row * ldc + col;
       float* ap = HAS_AUX ? aux + (long long)row * g.ldaux + col : nullptr;
-      float old[8], ax[8], bb[8];
-      if constexpr (HAS_BIAS) {
-        if (bvec && col + 8 <= N) {
-          const floatx4 b0 = *reinterpret_cast<const floatx4*>(bias + col), b1 = *reinterpret_cast<const floatx4*>(bias + col + 4);
-          bb[0] = b0[0]; bb[1] = b0[1]; bb[2] = b0[2]; bb[3] = b0[3]; bb[4] = b1[0]; bb[5] = b1[1]; bb[6] = b1[2]; bb[7] = b1[3];
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) bb[e] = col + e < N ? bias[col + e] : 0.f;
-        }
-      }
+      float old[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ax[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if constexpr (EPI == K3M_EPI_DGELU) {
-        if (full) {
-          const floatx4 x0 = *reinterpret_cast<const floatx4*>(ap), x1 = *reinterpret_cast<const floatx4*>(ap + 4);
-          ax[0] = x0[0]; ax[1] = x0[1]; ax[2] = x0[2]; ax[3] = x0[3]; ax[4] = x1[0]; ax[5] = x1[1]; ax[6] = x1[2]; ax[7] = x1[3];
-        } else {
+        if (full) ld8(ap, ax);
+        else
 #pragma unroll
           for (int e = 0; e < 8; ++e) ax[e] = col + e < N ? ap[e] : 0.f;
-        }
       }
       if (rd_old) {
-        if (full) {
-          const floatx4 o0 = *reinterpret_cast<const floatx4*>(cp), o1 = *reinterpret_cast<const floatx4*>(cp + 4);
-          old[0] = o0[0]; old[1] = o0[1]; old[2] = o0[2]; old[3] = o0[3]; old[4] = o1[0]; old[5] = o1[1]; old[6] = o1[2]; old[7] = o1[3];
-        } else {
+        if (full) ld8(cp, old);
+        else
 #pragma unroll
           for (int e = 0; e < 8; ++e) old[e] = col + e < N ? cp[e] : 0.f;
-        }
       }
       float o[8], pa[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        if constexpr (EPI == K3M_EPI_NONE) {
-          o[e] = alpha * v[e];
-        } else if constexpr (EPI == K3M_EPI_BIAS) {
-          o[e] = alpha * (v[e] + bb[e]);
-        } else if constexpr (EPI == K3M_EPI_BIAS_GELU) {
-          pa[e] = v[e] + bb[e];
-          o[e] = gelu_f(pa[e]);
-        } else if constexpr (EPI == K3M_EPI_DGELU) {
-          o[e] = alpha * v[e] * dgelu_f(ax[e]);
-        } else {
-          o[e] = sigmoid_f(v[e] + bb[e]);
-        }
-        if (rd_old) o[e] += beta * old[e];
-      }
+      epi_math<EPI>(v, bb, ax, old, alpha, beta, rd_old, o, pa);
       if (full) {
-        *reinterpret_cast<floatx4*>(cp) = floatx4{o[0], o[1], o[2], o[3]};
-        *reinterpret_cast<floatx4*>(cp + 4) = floatx4{o[4], o[5], o[6], o[7]};
-        if constexpr (EPI == K3M_EPI_BIAS_GELU) {
-          *reinterpret_cast<floatx4*>(ap) = floatx4{pa[0], pa[1], pa[2], pa[3]};
-          *reinterpret_cast<floatx4*>(ap + 4) = floatx4{pa[4], pa[5], pa[6], pa[7]};
-        }
+        st8(cp, o);
+        if constexpr (EPI == K3M_EPI_BIAS_GELU) st8(ap, pa);
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e)
@@ -323,6 +407,18 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, float
     }
     __syncthreads();
   }
+}
+
+// FAST = false: no separate branch-free interior path (kernels already at their register limit, where the
+// second copy of the pass sequence made the main loop spill: the 256x256 input-gradient walk)
+template <int TBM, int TBN, int WM, int WN, int EPI, int CAP = 2 * (TBM + TBN) * BK, class Hook = NoHook,
+          bool FAST = true>
+__device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, float* smem,
+                                         const floatx16 (&acc)[TBM / WM / 32][TBN / WN / 32], int slice = -1,
+                                         Hook hook = Hook()) {
+  const Acc32Ref<TBM / WM / 32, TBN / WN / 32> r{acc};
+  epilogue_r<TBM, TBN, WM, WN, EPI, CAP, Hook, Acc32Ref<TBM / WM / 32, TBN / WN / 32>, FAST>(g, m0, n0, smem, r, slice,
+                                                                                              hook);
 }
 
 template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, bool VEC, int EPI, int OCC>

@@ -218,7 +218,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_x6_persist_kernel(GemmGr
     auto hook = [&]() {
       if (more) lp.prefetch(grp.g[nxt.p], nxt);
     };
-    K3M_F32_NS::epilogue<TBM, TBN, WM, WN, EPI, WORDS>(grp.g[cur.p], cur.m0, cur.n0, smem, acc, cur.slice, hook);
+    K3M_F32_NS::epilogue<TBM, TBN, WM, WN, EPI, WORDS, decltype(hook), !(AK && !BK_)>(
+        grp.g[cur.p], cur.m0, cur.n0, smem, acc, cur.slice, hook);
     if (!more) break;   // every wave leaves here: the exit condition is uniform over the workgroup
     lp.prefetch2();
     u = nu;

@@ -240,10 +240,10 @@ class _Deferred(object):
     def __init__(self):
         self.jobs = []      # (ws pointer, out pointer, nslab, cols, accumulate)
         self.keep = []      # workspaces referenced until the flush
-        self.stream = torch.cuda.current_stream() if torch.cuda.is_available() else None
+        self.stream = stream() if torch.cuda.is_available() else None
 
     def active_here(self):
-        return self.stream is not None and torch.cuda.current_stream() == self.stream
+        return self.stream is not None and stream() == self.stream
 
     def add(self, ws_ptr, out, nslab, cols, accumulate=1):
         self.jobs.append((ws_ptr, ptr(out), nslab, cols, accumulate))
