@@ -679,6 +679,277 @@ size_t fwd_reg_lds(int lk, int hd) {
   return sizeof(float) * (2 * LK * hd + LK);
 }
 
+// ------------------------------------------------------------------ forward on the bf16 matrix cores
+// The register-softmax forward with both products in the bf16x6 form of gemm_x6_tile.h (fp32 operands
+// split exactly into three bf16 planes, the six leading partial products accumulated in fp32 on
+// v_mfma_f32_32x32x16_bf16: 2.67x the f32-MFMA rate at fp32 accuracy).  Structure as attn_fwd_reg_kernel:
+//   S^T = K Q^T    A = K rows from LDS (two 16-B reads per 8 head dims, split in registers), B = this
+//                  wave's Q block (prescaled, split once when it fits the register budget);
+//   softmax        unchanged (the 32x32x16 bf16 MFMA has the accumulator layout of the f32 one);
+//   O^T = V^T P^T  B = the dropped probabilities of one 16-key step straight from the accumulators,
+//                  split; A = V^T from a transposed LDS image [HD][LKP] (key chunk c of row d at
+//                  c ^ (d & (LKP/4 - 1))), whose 8 keys per lane half — the accumulator order
+//                  32kt + 16s + 8(e>>2) + 4h + (e&3) — are two 16-B reads.
+typedef __bf16 x6bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t x6u32x4 __attribute__((ext_vector_type(4)));
+typedef float x6float2 __attribute__((ext_vector_type(2)));
+typedef __bf16 x6bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t x6_pk(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((x6float2{a, b}), x6bf16x2));
+}
+// x = h + m + l exactly (8 floats -> three packed bf16x8 planes)
+__device__ __forceinline__ void x6_split8(const float (&x)[8], x6bf16x8& h, x6bf16x8& m, x6bf16x8& l) {
+  x6u32x4 H, Mm, L;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float a = x[2 * p], b = x[2 * p + 1];
+    const uint32_t hh = x6_pk(a, b);
+    const float r1a = a - __uint_as_float(hh << 16), r1b = b - __uint_as_float(hh & 0xffff0000u);
+    const uint32_t mm = x6_pk(r1a, r1b);
+    const float r2a = r1a - __uint_as_float(mm << 16), r2b = r1b - __uint_as_float(mm & 0xffff0000u);
+    H[p] = hh;
+    Mm[p] = mm;
+    L[p] = x6_pk(r2a, r2b);
+  }
+  h = __builtin_bit_cast(x6bf16x8, H);
+  m = __builtin_bit_cast(x6bf16x8, Mm);
+  l = __builtin_bit_cast(x6bf16x8, L);
+}
+// acc += a.b over the six leading plane products, smallest first
+__device__ __forceinline__ void x6_mma(floatx16& acc, const x6bf16x8& ah, const x6bf16x8& am, const x6bf16x8& al,
+                                       const x6bf16x8& bh, const x6bf16x8& bm, const x6bf16x8& bl) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+}
+
+__host__ __device__ constexpr int x6_lkp(int LK) { return LK <= 32 ? 32 : LK <= 64 ? 64 : 128; }
+
+template <int HD>
+__global__ __launch_bounds__(256, 2) void attn_fwd_x6_kernel(const float* __restrict__ q, long long ldq,
+                                                             const float* __restrict__ k, long long ldk,
+                                                             const float* __restrict__ v, long long ldv,
+                                                             const float* __restrict__ kmask, float* __restrict__ ctx,
+                                                             long long ldc, float* __restrict__ probs, int lq, int lk,
+                                                             int nh, float scale, float p_drop, uint64_t seed,
+                                                             uint64_t off) {
+  constexpr int NTH = 256, HH = HD / 2, NCH = HD / 4, NS = HH / 8;
+  constexpr int SWZ = (HD % 64 == 0) ? 15 : 7;    // K image: 16-byte chunk index XOR (key & SWZ)
+  constexpr int U = 8192 / 4 / NTH;               // staging chunks per thread and operand (LK*HD <= 8192)
+  constexpr bool QSPLIT = HD <= 96;               // Q planes held in registers (else split per use)
+  extern __shared__ float smem[];
+  const int s = blockIdx.x / nh, h = blockIdx.x % nh;
+  const int LK = (lk + 31) & ~31, nkt = LK >> 5;
+  const int LKP = x6_lkp(LK), VM = LKP / 4 - 1;
+  float* Ks = smem;              // [LK][HD]
+  float* Vt = Ks + LK * HD;      // [HD][LKP]
+  float* mk = Vt + HD * LKP;     // [LK] key mask in log2 units, -inf on padding keys
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
+  const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
+  const int hoff = h * HD;
+  const long long pbase = ((long long)s * nh + h) * lq * lk;
+  const int qi = 32 * w + cl;
+
+  // staging: K row-major (chunk-swizzled), V transposed (keys of one d contiguous), the mask
+  {
+    float4 kc[U], vc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = threadIdx.x + u * NTH;
+      const int j = e / NCH, c = e % NCH;                 // K: row-major chunks (coalesced)
+      const bool ok = e < LK * NCH && j < lk;
+      kc[u] = ok ? *reinterpret_cast<const float4*>(k + (krow0 + j) * ldk + hoff + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int jv = e % LK, cv = e / LK;                 // V: 64 consecutive keys per wave instruction
+      const bool okv = e < LK * NCH && jv < lk;
+      vc[u] = okv ? *reinterpret_cast<const float4*>(v + (krow0 + jv) * ldv + hoff + 4 * cv) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float mv = 0.f;
+    if (threadIdx.x < LK && kmask) mv = kmask[krow0 + min((int)threadIdx.x, lk - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = threadIdx.x + u * NTH;
+      if (e < LK * NCH) {
+        const int j = e / NCH, c = e % NCH;
+        *reinterpret_cast<float4*>(Ks + j * HD + 4 * (c ^ (j & SWZ))) = kc[u];
+        const int jv = e % LK, cv = e / LK;
+        const float vv[4] = {vc[u].x, vc[u].y, vc[u].z, vc[u].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int d = 4 * cv + i;
+          Vt[d * LKP + 4 * ((jv >> 2) ^ (d & VM)) + (jv & 3)] = vv[i];
+        }
+      }
+    }
+    if (threadIdx.x < LK) mk[threadIdx.x] = (int)threadIdx.x < lk ? mv * LOG2E : -INFINITY;
+  }
+  float qr[HH];
+  {
+    const float sl = scale * LOG2E;
+    const bool ok = qi < lq;
+    const float* src = q + (qrow0 + (ok ? qi : 0)) * ldq + hoff + kl * HH;
+#pragma unroll
+    for (int c = 0; c < HH / 4; ++c) {
+      const float4 t = ok ? *reinterpret_cast<const float4*>(src + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      qr[4 * c] = t.x * sl;
+      qr[4 * c + 1] = t.y * sl;
+      qr[4 * c + 2] = t.z * sl;
+      qr[4 * c + 3] = t.w * sl;
+    }
+  }
+  x6bf16x8 qh[QSPLIT ? NS : 1], qm[QSPLIT ? NS : 1], ql[QSPLIT ? NS : 1];
+  if constexpr (QSPLIT) {
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+      float t[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t[e] = qr[8 * st + e];
+      x6_split8(t, qh[st], qm[st], ql[st]);
+    }
+  }
+  __syncthreads();
+  if (32 * w >= lq) return;   // no queries for this wave (no barrier follows)
+
+  // S^T tiles, started at the key mask: head dims kl*HH + 8st + e on both operands
+  floatx16 acc[4];
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) {
+    if (kt < nkt) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const float4 m4 = *reinterpret_cast<const float4*>(mk + 32 * kt + 8 * a + 4 * kl);
+        acc[kt][4 * a] = m4.x;
+        acc[kt][4 * a + 1] = m4.y;
+        acc[kt][4 * a + 2] = m4.z;
+        acc[kt][4 * a + 3] = m4.w;
+      }
+      const int key = 32 * kt + cl;
+      const float* krow = Ks + key * HD;
+      const int sw = key & SWZ;
+#pragma unroll
+      for (int st = 0; st < NS; ++st) {
+        const int c0 = (kl * HH + 8 * st) >> 2;
+        const float4 a0 = *reinterpret_cast<const float4*>(krow + 4 * (c0 ^ sw));
+        const float4 a1 = *reinterpret_cast<const float4*>(krow + 4 * ((c0 + 1) ^ sw));
+        const float ka[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        x6bf16x8 ah, am, al;
+        x6_split8(ka, ah, am, al);
+        if constexpr (QSPLIT) {
+          x6_mma(acc[kt], ah, am, al, qh[st], qm[st], ql[st]);
+        } else {
+          float t[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) t[e] = qr[8 * st + e];
+          x6bf16x8 bh, bm, bl;
+          x6_split8(t, bh, bm, bl);
+          x6_mma(acc[kt], ah, am, al, bh, bm, bl);
+        }
+      }
+    }
+  }
+
+  // softmax over the keys of query qi, in the accumulators (as attn_fwd_reg_kernel)
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+    if (kt < nkt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, acc[kt][r]);
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sm = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+    if (kt < nkt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        acc[kt][r] = exp2f(acc[kt][r] - mx);
+        sm += acc[kt][r];
+      }
+  sm += __shfl_xor(sm, 32, 64);
+  {
+    const float inv = __builtin_amdgcn_rcpf(sm);
+    const K3mDrop dr = k3m_drop_init(seed, p_drop);
+    const bool qok = qi < lq;
+    const long long prow = pbase + (long long)(qok ? qi : 0) * lk;
+    const bool vec = (lk & 3) == 0;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      if (kt < nkt) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          const int j0 = 32 * kt + 8 * a + 4 * kl;
+          float p4[4];
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int j = j0 + b;
+            p4[b] = acc[kt][4 * a + b] * inv;
+            acc[kt][4 * a + b] = j < lk ? p4[b] * k3m_drop(dr, off + prow + j) : 0.f;
+          }
+          if (qok) {
+            if (vec && j0 < lk) {
+              *reinterpret_cast<float4*>(probs + prow + j0) = make_float4(p4[0], p4[1], p4[2], p4[3]);
+            } else if (!vec) {
+#pragma unroll
+              for (int b = 0; b < 4; ++b)
+                if (j0 + b < lk) probs[prow + j0 + b] = p4[b];
+            }
+          }
+        }
+      }
+    }
+  }
+
+  // O^T = V^T P^T: 16-key steps (kt, s2); lane half kl carries keys 32kt + 16 s2 + 8(e>>2) + 4kl + (e&3)
+  floatx16 o[HD / 32];
+#pragma unroll
+  for (int dt = 0; dt < HD / 32; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) {
+    if (kt < nkt) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        float pv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pv[e] = acc[kt][8 * s2 + e];
+        x6bf16x8 ph, pm, pl;
+        x6_split8(pv, ph, pm, pl);
+        const int ch = 8 * kt + 4 * s2 + kl;   // key chunk of e = 0..3 (e = 4..7: ch + 2)
+#pragma unroll
+        for (int dt = 0; dt < HD / 32; ++dt) {
+          const int d = 32 * dt + cl;
+          const float* vrow = Vt + d * LKP;
+          const float4 v0 = *reinterpret_cast<const float4*>(vrow + 4 * (ch ^ (d & VM)));
+          const float4 v1 = *reinterpret_cast<const float4*>(vrow + 4 * ((ch + 2) ^ (d & VM)));
+          const float va[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+          x6bf16x8 vh, vm, vl;
+          x6_split8(va, vh, vm, vl);
+          x6_mma(o[dt], vh, vm, vl, ph, pm, pl);
+        }
+      }
+    }
+  }
+  if (qi < lq) {
+    float* dst = ctx + (qrow0 + qi) * ldc + hoff + 4 * kl;
+#pragma unroll
+    for (int dt = 0; dt < HD / 32; ++dt)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        *reinterpret_cast<float4*>(dst + 32 * dt + 8 * a) =
+            make_float4(o[dt][4 * a], o[dt][4 * a + 1], o[dt][4 * a + 2], o[dt][4 * a + 3]);
+  }
+}
+
+size_t fwd_x6_lds(int lk, int hd) {
+  const int LK = (lk + 31) & ~31;
+  return sizeof(float) * ((size_t)LK * hd + (size_t)hd * x6_lkp(LK) + LK);
+}
+
 // 16-byte global -> LDS copy (global_load_lds_dwordx4): the LDS destination is the wave-uniform base
 // plus 16 * lane
 __device__ __forceinline__ void glds16(const float* g, float* lds_base) {
@@ -989,6 +1260,10 @@ void launch_bwd(const void* dctx, long long ldc, const void* o, long long ldo, c
 // the register-softmax forward serves fp32 heads whose K and V fit 2 workgroups per CU
 static const bool kAttnFwdReg = k3m_env_flag("K3M_ATTN_FWD_REG", true);
 
+// the forward's two products on the bf16 matrix cores (bf16x6, attn_fwd_x6_kernel); K3M_ATTN_X6=0 keeps
+// the f32-MFMA register kernel
+static const bool kAttnX6 = k3m_env_flag("K3M_ATTN_X6", true);
+
 template <int HD>
 void launch_fwd_reg(const void* q, long long ldq, const void* k, long long ldk, const void* v, long long ldv,
                     const float* kmask, void* ctx, long long ldc, float* probs, int nseq, int lq, int lk, int nh,
@@ -996,7 +1271,14 @@ void launch_fwd_reg(const void* q, long long ldq, const void* k, long long ldk, 
   static bool done = false;
   if (!done) {
     (void)hipFuncSetAttribute((const void*)attn_fwd_reg_kernel<HD>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_x6_kernel<HD>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     done = true;
+  }
+  if (kAttnX6) {
+    hipLaunchKernelGGL(attn_fwd_x6_kernel<HD>, dim3(nseq * nh), dim3(256), fwd_x6_lds(lk, HD), st, (const float*)q,
+                       ldq, (const float*)k, ldk, (const float*)v, ldv, kmask, (float*)ctx, ldc, probs, lq, lk, nh, scale,
+                       p_drop, seed, off);
+    return;
   }
   hipLaunchKernelGGL(attn_fwd_reg_kernel<HD>, dim3(nseq * nh), dim3(256), fwd_reg_lds(lk, HD), st, (const float*)q, ldq,
                      (const float*)k, ldk, (const float*)v, ldv, kmask, (float*)ctx, ldc, probs, lq, lk, nh, scale, p_drop,
