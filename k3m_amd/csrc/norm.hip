@@ -331,15 +331,41 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restric
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
-  const long long id = ids[row], t = tt[row];
-  const int l = row % len;
+  (void)tt;
+  (void)dpos;
+  (void)dtyp;
+  (void)len;
+  const long long id = ids[row];
   const long long base = (long long)row * cols;
-  for (int c = lane; c < cols; c += 64) {
-    const float g = to_f(ds[base + c]);
-    if (id != 0) atomicAdd(dword + id * cols + c, g);
-    atomicAdd(dpos + (long long)l * cols + c, g);
-    atomicAdd(dtyp + t * cols + c, g);
+  if (id == 0) return;   // padding_idx = 0 (vilbert_k3m.py:344): no gradient
+  for (int c = lane; c < cols; c += 64) atomicAdd(dword + id * cols + c, to_f(ds[base + c]));
+}
+
+// Position and token-type gradients without contended atomics: the 36-128 position rows and the two
+// type rows receive a term from EVERY token, so one atomic per (token, column) serialised thousands
+// of adds on each address (embedding backward at 0.03 of its HBM roofline, profiles/r1_kernel_roofline_v2.txt).
+// Here a block owns (position l, 256 columns) and sums the nseq tokens at that position in registers:
+// dpos[l] gets a plain read-modify-write (one owner), the two type rows one atomic per block and column.
+template <typename T>
+__global__ __launch_bounds__(256) void embed_bwd_pos_type_kernel(const int64_t* __restrict__ tt,
+                                                                 const T* __restrict__ ds, float* dpos, float* dtyp,
+                                                                 int nseq, int len, int cols) {
+  const int l = blockIdx.x;
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float sp = 0.f, s0 = 0.f, s1 = 0.f;
+  for (int s = 0; s < nseq; ++s) {
+    const long long row = (long long)s * len + l;
+    const float g = to_f(ds[row * cols + c]);
+    const long long t = tt[row];
+    sp += g;
+    if (t == 0) s0 += g;
+    else if (t == 1) s1 += g;
+    else atomicAdd(dtyp + t * cols + c, g);   // type_vocab_size > 2
   }
+  dpos[(long long)l * cols + c] += sp;
+  atomicAdd(dtyp + c, s0);
+  atomicAdd(dtyp + cols + c, s1);
 }
 
 // ------------------------------------------------------------------ column sums
@@ -572,6 +598,9 @@ extern "C" int k3m_embed_bwd(const int64_t* ids, const int64_t* tt, const void* 
   if (rows == 0) return 0;
   DISPATCH_T(dtype, hipLaunchKernelGGL(embed_bwd_kernel<T>, dim3(k3m_cdiv(rows, 4)), dim3(256), 0, st, ids, tt,
                                        (const T*)ds, dword, dpos, dtype_, rows, len, hidden));
+  K3M_CHECK_LAUNCH();
+  DISPATCH_T(dtype, hipLaunchKernelGGL(embed_bwd_pos_type_kernel<T>, dim3(len, k3m_cdiv(hidden, 256)), dim3(256), 0, st,
+                                       tt, (const T*)ds, dpos, dtype_, nseq, len, hidden));
   K3M_CHECK_LAUNCH();
   return 0;
 }

@@ -165,12 +165,18 @@ def linear(x, W, b=None, out=None, epi=None, aux=None, alpha=1.0, beta=0.0, out_
 
 
 def linear_dgrad(dy, W, dx=None, beta=0.0, dgelu_aux=None, alpha=1.0):
-    """dx (+)= dy . W (optionally * gelu'(aux)); dy [M,N], W [N,K]."""
+    """dx (+)= dy . W (optionally * gelu'(aux)); dy [M,N], W [N,K].  A plain input gradient whose output
+    fills few tiles but whose reduction is long (the tied MLM decoder: 1,536 labelled rows x 768 over the
+    21,128-word vocabulary) is split over K like a weight gradient (fp32 slabs reduced with alpha/beta)."""
     M, N = dy.shape
     K = W.shape[1]
     if dx is None:
         dx = torch.empty((M, K), dtype=dy.dtype, device=dy.device)
     epi = L.EPI_DGELU if dgelu_aux is not None else L.EPI_NONE
+    s = _splitk(M, K, N, dy.dtype) if (epi == L.EPI_NONE and dx.dtype == torch.float32 and N >= 8192) else 1
+    if s > 1:
+        ws = torch.empty((s * M * K,), dtype=torch.float32, device=dy.device)
+        return gemm(dy, 0, W, 0, dx, M, K, N, epi, None, None, alpha, beta, s, ws)
     return gemm(dy, 0, W, 0, dx, M, K, N, epi, None, dgelu_aux, alpha, beta)
 
 
