@@ -72,6 +72,11 @@ int k3m_gemm(const K3mGemm* g, hipStream_t stream);
  * reduces them later with k3m_slab_reduce_batch (nslab = splitk, cols = m*n, requires ldc == n,
  * alpha == 1; the engine batches these with the LayerNorm / bias slabs of a whole encoder block). */
 #define K3M_GEMM_SLABS_ONLY 0x100
+/* OR-ed into K3mGemm.epilogue of a K3M_EPI_DGELU GEMM (splitk <= 1, beta == 0): the kernel also writes the
+ * column sums of its output C into ws, one fp32 slab per 32-row group (ws[r/32][n], ceil(m/32) slabs of n
+ * floats) — the bias gradient of the Linear that C feeds, without re-reading C (replaces k3m_colsum on it).
+ * The caller reduces the slabs with k3m_slab_reduce_batch (nslab = ceil(m/32), cols = n). */
+#define K3M_GEMM_COLSUM_SLABS 0x200
 /* Up to 8 INDEPENDENT problems in one launch (no problem may read another's output).  When all share
  * one kernel template (fp32 operands on the bf16x6 path, same a_trans / b_trans / epilogue, 16-B
  * aligned) they run as one grid of 256x128 tiles — the co-attention blocks' six small GEMMs per

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("K3M_LIB") or os.path.join(_HERE, "libk3m_hip.so")
 F32, BF16 = 0, 1
 EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_DGELU, EPI_BIAS_SIGMOID = 0, 1, 2, 3, 4
 GEMM_SLABS_ONLY = 0x100   # K3M_GEMM_SLABS_ONLY: split-K slabs left for k3m_slab_reduce_batch
+GEMM_COLSUM_SLABS = 0x200   # K3M_GEMM_COLSUM_SLABS: dGELU output column sums as 32-row slabs in ws
 F32_SPLIT_BF16X6, F32_MFMA_F32 = 0, 1
 ADAM_ZERO_GRAD, ADAM_APEX, ADAM_APEX_BIAS_CORRECTION = 1, 2, 4
 

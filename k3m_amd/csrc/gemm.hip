@@ -164,16 +164,21 @@ int launch_x6_persistent_one(const K3mGemm& g, bool t256, bool ak, bool bk, hipS
 }
 }  // namespace
 
-int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st, bool slabs_only);  // gemm_bf16.hip
+int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st, bool slabs_only, bool colsum);  // gemm_bf16.hip
 int k3m_gemm_bf16_grouped_impl(const K3mGemm* gs, int count, hipStream_t st, bool* handled, const bool* slabs_only);
+// (the grouped problems carry their COLSUM_SLABS request as a non-null ws with splitk <= 1)
 
 extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
   if (!gp) return K3M_EINVAL;
   const bool slabs_only = (gp->epilogue & K3M_GEMM_SLABS_ONLY) != 0;
+  const bool colsum = (gp->epilogue & K3M_GEMM_COLSUM_SLABS) != 0;
   K3mGemm gl = *gp;
-  gl.epilogue &= ~K3M_GEMM_SLABS_ONLY;
+  gl.epilogue &= ~(K3M_GEMM_SLABS_ONLY | K3M_GEMM_COLSUM_SLABS);
+  // kernels read a non-split ws as the COLSUM_SLABS request
+  if (!colsum && gl.splitk <= 1) gl.ws = nullptr;
   const K3mGemm& g = gl;
   K3M_ARG(!slabs_only || (g.splitk > 1 && g.ldc == g.n));
+  K3M_ARG(!colsum || (g.epilogue == K3M_EPI_DGELU && g.splitk <= 1 && g.beta == 0.f && g.ws));
   K3M_ARG(g.m >= 0 && g.n >= 0 && g.k >= 0);
   if (g.m == 0 || g.n == 0) return 0;
   K3M_ARG(g.dtype == K3M_F32 || g.dtype == K3M_BF16);
@@ -183,7 +188,7 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
   K3M_ARG(g.epilogue == K3M_EPI_NONE || g.epilogue == K3M_EPI_DGELU || g.bias);
   K3M_ARG((g.epilogue != K3M_EPI_BIAS_GELU && g.epilogue != K3M_EPI_DGELU) || g.aux);
   K3M_ARG(g.f32_algo == K3M_F32_SPLIT_BF16X6 || g.f32_algo == K3M_F32_MFMA_F32);
-  if (g.dtype == K3M_BF16) return k3m_gemm_bf16_impl(g, st, slabs_only);
+  if (g.dtype == K3M_BF16) return k3m_gemm_bf16_impl(g, st, slabs_only, colsum);
   // A: K-contiguous iff a_trans == 0; B: K-contiguous iff b_trans == 1
   const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
   const bool av = aligned16(g.a) && (g.lda % 4 == 0) && ((ak ? g.k : g.m) % 4 == 0);
@@ -261,12 +266,15 @@ extern "C" int k3m_gemm_grouped(const K3mGemm* gs_in, int count, hipStream_t st)
   if (count == 0) return 0;
   // K3M_GEMM_SLABS_ONLY per problem: stripped here, remembered for the split-K reductions below
   K3mGemm gs[k3m_x6::GROUP_MAX];
-  bool slabs_only[k3m_x6::GROUP_MAX];
+  bool slabs_only[k3m_x6::GROUP_MAX], colsum[k3m_x6::GROUP_MAX];
   for (int i = 0; i < count; ++i) {
     gs[i] = gs_in[i];
     slabs_only[i] = (gs[i].epilogue & K3M_GEMM_SLABS_ONLY) != 0;
-    gs[i].epilogue &= ~K3M_GEMM_SLABS_ONLY;
+    colsum[i] = (gs[i].epilogue & K3M_GEMM_COLSUM_SLABS) != 0;
+    gs[i].epilogue &= ~(K3M_GEMM_SLABS_ONLY | K3M_GEMM_COLSUM_SLABS);
+    if (!colsum[i] && gs[i].splitk <= 1) gs[i].ws = nullptr;
     K3M_ARG(!slabs_only[i] || (gs[i].splitk > 1 && gs[i].ldc == gs[i].n));
+    K3M_ARG(!colsum[i] || (gs[i].epilogue == K3M_EPI_DGELU && gs[i].splitk <= 1 && gs[i].beta == 0.f && gs[i].ws));
   }
   // one template for the whole group: same layout, epilogue, dtype, algorithm, 16-B aligned operands
   const K3mGemm& g0 = gs[0];
@@ -298,6 +306,7 @@ extern "C" int k3m_gemm_grouped(const K3mGemm* gs_in, int count, hipStream_t st)
     for (int i = 0; i < count; ++i) {
       K3mGemm gi = gs[i];
       if (slabs_only[i]) gi.epilogue |= K3M_GEMM_SLABS_ONLY;
+      if (colsum[i]) gi.epilogue |= K3M_GEMM_COLSUM_SLABS;
       const int rc = k3m_gemm(&gi, st);
       if (rc) return rc;
     }
@@ -307,7 +316,8 @@ extern "C" int k3m_gemm_grouped(const K3mGemm* gs_in, int count, hipStream_t st)
     const K3mGemm& g = grp.g[i];
     K3M_ARG(g.a && g.b && g.c && g.k >= 0);
     K3M_ARG(g.splitk <= 1 || (g.epilogue == K3M_EPI_NONE && g.ws));
-    K3M_ARG(g.epilogue == K3M_EPI_NONE || g.epilogue == K3M_EPI_DGELU || g.bias);
+    K3M_ARG(g.epilogue == K3M_EPI_NONE || g.epilogue == K3M_EPI_DGELU || g.bias);   // (ws of a non-split
+                                                                                    // problem: its colsum slabs)
     K3M_ARG((g.epilogue != K3M_EPI_BIAS_GELU && g.epilogue != K3M_EPI_DGELU) || g.aux);
   }
   if (live == 0) return 0;

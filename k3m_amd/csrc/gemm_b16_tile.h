@@ -22,6 +22,7 @@
 //    bias+sigmoid / alpha, beta; split-K writes raw fp32 slabs reduced by the caller.
 #pragma once
 #include "common.h"
+#include "gemm_f32_tile.h"
 
 #include <type_traits>
 
@@ -435,6 +436,10 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint1
   }
   const bool rd_old = CAN_OLD && beta != 0.f;
   auto row_of = [&](int grp, int ps) { return m0 + wm + 32 * grp + ps * RPP + lr; };
+  // K3M_GEMM_COLSUM_SLABS (dGELU only, as in k3m_f32::epilogue_r): column sums of the STORED values of C
+  constexpr bool CSUM = EPI == K3M_EPI_DGELU;
+  float* const cws = (CSUM && !split) ? g.ws : nullptr;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (cvec && m0 + TBM <= M && n0 + TBN <= N) {
     auto body = [&](auto old_tag) {
       constexpr bool OLD = decltype(old_tag)::value;
@@ -471,6 +476,14 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint1
           epi_math8<EPI>(v, bb, ax, old, alpha, beta, OLD, o, pa);
           store8(C + row * ldc + col, o);
           if constexpr (EPI == K3M_EPI_BIAS_GELU) store8(aux + row * g.ldaux + col, pa);
+          if constexpr (CSUM) {
+            if (cws)
+#pragma unroll
+              for (int e = 0; e < 8; ++e) cs[e] += to_f(from_f<CT>(o[e]));
+          }
+        }
+        if constexpr (CSUM) {
+          if (cws) K3M_F32_NS::colsum_flush<LPR>(cs, cws, (m0 + wm + 32 * grp) >> 5, N, col, lane, true);
         }
         __syncthreads();
       }
@@ -510,6 +523,11 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint1
       }
       float o[8], pa[8];
       epi_math8<EPI>(v, bb, ax, old, alpha, beta, rd_old, o, pa);
+      if constexpr (CSUM) {
+        if (cws)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cs[e] += col + e < N ? to_f(from_f<CT>(o[e])) : 0.f;
+      }
       if (full) {
         store8(cp, o);
         if constexpr (EPI == K3M_EPI_BIAS_GELU) store8(ap, pa);
@@ -521,6 +539,9 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint1
             if constexpr (EPI == K3M_EPI_BIAS_GELU) ap[e] = from_f<CT>(pa[e]);
           }
       }
+    }
+    if constexpr (CSUM) {
+      if (cws) K3M_F32_NS::colsum_flush<LPR>(cs, cws, (m0 + wm + 32 * grp) >> 5, N, col, lane, m0 + wm + 32 * grp < M);
     }
     __syncthreads();
   }

@@ -567,20 +567,44 @@ const bool kBig = k3m_env_flag("K3M_BF16_BIG", true);
 
 }  // namespace
 
+// K3M_GEMM_COLSUM_SLABS for the kernels whose epilogue does not fuse it: 32-row column sums of C
+template <typename CT>
+__global__ __launch_bounds__(256) void colsum32_kernel(const CT* __restrict__ c, long long ldc, int m, int n,
+                                                       float* __restrict__ ws) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= n) return;
+  const int r0 = blockIdx.y * 32, r1 = min(m, r0 + 32);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += to_f(c[(long long)r * ldc + col]);
+  ws[(long long)blockIdx.y * n + col] = s;
+}
+
 // Called by k3m_gemm (gemm.hip) for dtype == K3M_BF16; arguments already validated there.
-int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st, bool slabs_only) {
+int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st, bool slabs_only, bool colsum) {
   K3M_ARG(g.splitk <= 1 || g.c_dtype == K3M_F32);
   const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
   const bool vec = vec_of(g);
   int rc;
   const long long nb256 = nb_of(g, 256, 256), nb128 = nb_of(g, 256, 128);
+  bool fused = false;   // the large-tile epilogue writes the COLSUM_SLABS itself
   if (kBig && big_ok(g, vec) && nb128 >= 160) {
     rc = big_prefers_256(nb256) ? big_launch<256, 256, 2, 4>(g, st) : big_launch<256, 128, 4, 2>(g, st);
+    fused = true;
   } else {
     rc = g.c_dtype == K3M_F32 ? launch_ct<float>(g, ak, bk, vec, st) : launch_ct<bf16_t>(g, ak, bk, vec, st);
   }
   if (rc) return rc;
   K3M_CHECK_LAUNCH();
+  if (colsum && !fused) {
+    const dim3 grid((g.n + 255) / 256, (g.m + 31) / 32);
+    if (g.c_dtype == K3M_F32)
+      hipLaunchKernelGGL(colsum32_kernel<float>, grid, dim3(256), 0, st, static_cast<const float*>(g.c), g.ldc, g.m,
+                         g.n, g.ws);
+    else
+      hipLaunchKernelGGL(colsum32_kernel<bf16_t>, grid, dim3(256), 0, st, static_cast<const bf16_t*>(g.c), g.ldc, g.m,
+                         g.n, g.ws);
+    K3M_CHECK_LAUNCH();
+  }
   return slabs_only ? 0 : reduce_splits(g, st);   // K3M_GEMM_SLABS_ONLY: the caller reduces the slabs
 }
 

@@ -266,6 +266,30 @@ __device__ __forceinline__ void epi_math(const float (&v)[8], const float (&bb)[
   }
 }
 
+// K3M_GEMM_COLSUM_SLABS: column sums of one 32-row group of C.  Lanes sharing columns (lane % LPR) are
+// reduced over the row lanes by XOR shuffles; lanes 0..LPR-1 write the group's slab row ws[slab][col..col+7].
+template <int LPR>
+__device__ __forceinline__ void colsum_flush(float (&cs)[8], float* ws, int slab, int N, int col, int lane,
+                                             bool live) {
+#pragma unroll
+  for (int off = LPR; off < 64; off <<= 1)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[e] += __shfl_xor(cs[e], off, 64);
+  if (live && lane < LPR && col < N) {
+    float* p = ws + (long long)slab * N + col;
+    if (col + 8 <= N && (N & 3) == 0) {
+      *reinterpret_cast<floatx4*>(p) = floatx4{cs[0], cs[1], cs[2], cs[3]};
+      *reinterpret_cast<floatx4*>(p + 4) = floatx4{cs[4], cs[5], cs[6], cs[7]};
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (col + e < N) p[e] = cs[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) cs[e] = 0.f;
+}
+
 // Global traffic of the epilogue is kept out of its own way.  vmcnt counts loads AND stores in issue
 // order, so a load issued after a store cannot be waited for without waiting for that store: a
 // per-pass bias load drained every store of the previous pass before the next pass could compute
@@ -311,6 +335,12 @@ __device__ __forceinline__ void epilogue_r(const K3mGemm& g, int m0, int n0, flo
     for (int e = 0; e < 8; ++e) asm volatile("" ::"v"(bb[e]));   // waited for here, before any store
   }
   auto row_of = [&](int i, int ps) { return m0 + wm + 32 * i + ps * RPP + lr; };
+  // the dGELU input gradient can also leave the column sums of its output (the bias gradient of the Linear
+  // it feeds, K3M_GEMM_COLSUM_SLABS: ws = [ceil(m/32)][n] slabs, one per 32-row group; k3m_gemm passes ws
+  // only when the flag is set)
+  constexpr bool CSUM = EPI == K3M_EPI_DGELU;
+  float* const cws = (CSUM && !split) ? g.ws : nullptr;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   // passes the per-pass loads run ahead (their registers: RING x 8 floats per load stream)
   constexpr int RING = K3M_EPI_RING;
   const bool interior = FAST && cvec && m0 + TBM <= M && n0 + TBN <= N;
@@ -353,6 +383,14 @@ __device__ __forceinline__ void epilogue_r(const K3mGemm& g, int m0, int n0, flo
           epi_math<EPI>(v, bb, ax, old, alpha, beta, OLD, o, pa);
           st8(C + row * ldc + col, o);
           if constexpr (EPI == K3M_EPI_BIAS_GELU) st8(aux + row * g.ldaux + col, pa);
+          if constexpr (CSUM) {
+            if (cws)
+#pragma unroll
+              for (int e = 0; e < 8; ++e) cs[e] += o[e];
+          }
+        }
+        if constexpr (CSUM) {
+          if (cws) colsum_flush<LPR>(cs, cws, (m0 + wm + 32 * i) >> 5, N, col, lane, true);
         }
         __syncthreads();
       }
@@ -393,6 +431,11 @@ __device__ __forceinline__ void epilogue_r(const K3mGemm& g, int m0, int n0, flo
       }
       float o[8], pa[8];
       epi_math<EPI>(v, bb, ax, old, alpha, beta, rd_old, o, pa);
+      if constexpr (CSUM) {
+        if (cws)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cs[e] += col + e < N ? o[e] : 0.f;
+      }
       if (full) {
         st8(cp, o);
         if constexpr (EPI == K3M_EPI_BIAS_GELU) st8(ap, pa);
@@ -404,6 +447,9 @@ __device__ __forceinline__ void epilogue_r(const K3mGemm& g, int m0, int n0, flo
             if constexpr (EPI == K3M_EPI_BIAS_GELU) ap[e] = pa[e];
           }
       }
+    }
+    if constexpr (CSUM) {
+      if (cws) colsum_flush<LPR>(cs, cws, (m0 + wm + 32 * i) >> 5, N, col, lane, m0 + wm + 32 * i < M);
     }
     __syncthreads();
   }

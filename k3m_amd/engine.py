@@ -133,8 +133,9 @@ class Lin(object):
         """bias_done: the bias gradient was already accumulated by dy's producer (k3m_ln_bwd dxsum)."""
         ops.linear_wgrad(dy, x, self.gW, None if bias_done else self.gb, alpha=alpha)
 
-    def dgrad(self, dy, dx=None, beta=0.0, dgelu_aux=None, alpha=1.0):
-        return ops.linear_dgrad(dy, self._w(dy), dx=dx, beta=beta, dgelu_aux=dgelu_aux, alpha=alpha)
+    def dgrad(self, dy, dx=None, beta=0.0, dgelu_aux=None, alpha=1.0, colsum_out=None):
+        return ops.linear_dgrad(dy, self._w(dy), dx=dx, beta=beta, dgelu_aux=dgelu_aux, alpha=alpha,
+                                colsum_out=colsum_out)
 
 
 class LN(object):
@@ -192,8 +193,8 @@ class FFN(object):
         dh = dh_out if dh_out is not None else torch.empty_like(h)
         do = self.tail.bwd(dy, tsv, dh, dxsum=self.o.gb)
         self.o.wgrad(do, f, bias_done=True)
-        du = self.o.dgrad(do, dgelu_aux=u)
-        self.i.wgrad(du, h)
+        du = self.o.dgrad(do, dgelu_aux=u, colsum_out=self.i.gb)   # + intermediate bias gradient
+        self.i.wgrad(du, h, bias_done=True)
         self.i.dgrad(du, dx=dh, beta=1.0)
         return dh
 
@@ -304,9 +305,9 @@ class BertLayerOp(object):
         dh1 = torch.empty_like(h1)
         do = self.ffn.tail.bwd(dy, ts2, dh1, dxsum=self.ffn.o.gb)
         self.ffn.o.wgrad(do, f, bias_done=True)
-        du = self.ffn.o.dgrad(do, dgelu_aux=u)
+        du = self.ffn.o.dgrad(do, dgelu_aux=u, colsum_out=self.ffn.i.gb)
         yield
-        self.ffn.i.wgrad(du, h1)
+        self.ffn.i.wgrad(du, h1, bias_done=True)
         self.ffn.i.dgrad(du, dx=dh1, beta=1.0)
         yield
         dx = torch.empty_like(x)
@@ -413,11 +414,11 @@ class ConnectionOp(object):
         do2 = self.f2.tail.bwd(dy2, ts2, dh2, dxsum=self.f2.o.gb)
         self.f1.o.wgrad(do1, g1, bias_done=True)
         self.f2.o.wgrad(do2, g2, bias_done=True)
-        du1 = self.f1.o.dgrad(do1, dgelu_aux=u1)
-        du2 = self.f2.o.dgrad(do2, dgelu_aux=u2)
+        du1 = self.f1.o.dgrad(do1, dgelu_aux=u1, colsum_out=self.f1.i.gb)
+        du2 = self.f2.o.dgrad(do2, dgelu_aux=u2, colsum_out=self.f2.i.gb)
         yield
-        self.f1.i.wgrad(du1, h1)
-        self.f2.i.wgrad(du2, h2)
+        self.f1.i.wgrad(du1, h1, bias_done=True)
+        self.f2.i.wgrad(du2, h2, bias_done=True)
         self.f1.i.dgrad(du1, dx=dh1, beta=1.0)
         self.f2.i.dgrad(du2, dx=dh2, beta=1.0)
         yield

@@ -37,6 +37,7 @@ class _Grouper(object):
     def __init__(self):
         self.pending = []
         self.after = []   # non-GEMM work that must wait for the block's side-stream branches
+        self.post = []    # work that reads a GEMM output of the block: runs after the launches
 
     def flush(self):
         after, self.after = self.after, []
@@ -56,6 +57,9 @@ class _Grouper(object):
                 chunk = items[i:i + GROUP_MAX]
                 arr = (L.K3mGemm * len(chunk))(*[g for g, _ in chunk])
                 call("k3m_gemm_grouped", L.C.cast(arr, L.C.c_void_p), len(chunk), stream())
+        post, self.post = self.post, []
+        for fn in post:
+            fn()
 
 
 GROUP_MAX = 8
@@ -164,7 +168,16 @@ def linear(x, W, b=None, out=None, epi=None, aux=None, alpha=1.0, beta=0.0, out_
     return gemm(x, 0, W, 1, out, M, N, K, epi, b, aux, alpha, beta)
 
 
-def linear_dgrad(dy, W, dx=None, beta=0.0, dgelu_aux=None, alpha=1.0):
+def dgrad_colsum_ok(dy, beta=0.0):
+    """Whether an input gradient with the dGELU epilogue can leave its bias-gradient column sums as deferred
+    slabs (K3M_GEMM_COLSUM_SLABS) instead of a separate k3m_colsum pass over its output."""
+    return DGRAD_COLSUM and DEFER and _deferred is not None and beta == 0.0 and _deferred.active_here()
+
+
+DGRAD_COLSUM = os.environ.get("K3M_DGRAD_COLSUM", "1") != "0"   # A/B knob
+
+
+def linear_dgrad(dy, W, dx=None, beta=0.0, dgelu_aux=None, alpha=1.0, colsum_out=None):
     """dx (+)= dy . W (optionally * gelu'(aux)); dy [M,N], W [N,K].  A plain input gradient whose output
     fills few tiles but whose reduction is long (the tied MLM decoder: 1,536 labelled rows x 768 over the
     21,128-word vocabulary) is split over K like a weight gradient (fp32 slabs reduced with alpha/beta)."""
@@ -177,6 +190,21 @@ def linear_dgrad(dy, W, dx=None, beta=0.0, dgelu_aux=None, alpha=1.0):
     if s > 1:
         ws = torch.empty((s * M * K,), dtype=torch.float32, device=dy.device)
         return gemm(dy, 0, W, 0, dx, M, K, N, epi, None, None, alpha, beta, s, ws)
+    if colsum_out is not None:
+        # colsum_out += column sums of dx (the bias gradient of the Linear dx feeds): from the epilogue as
+        # 32-row slabs joining the deferred reduction, or by a separate pass when that is not possible
+        if epi == L.EPI_DGELU and dgrad_colsum_ok(dy, beta):
+            ns = (M + 31) // 32
+            ws = torch.empty((ns * K,), dtype=torch.float32, device=dy.device)
+            _deferred.keep.append(ws)
+            _deferred.add(ptr(ws), colsum_out, ns, K)
+            return gemm(dy, 0, W, 0, dx, M, K, N, epi | L.GEMM_COLSUM_SLABS, None, dgelu_aux, alpha, beta, 1, ws)
+        gemm(dy, 0, W, 0, dx, M, K, N, epi, None, dgelu_aux, alpha, beta)
+        if _grouper is not None:   # the GEMM is still pending: sum its output after the group's launches
+            _grouper.post.append(lambda: colsum(dx, colsum_out, accumulate=True))
+        else:
+            colsum(dx, colsum_out, accumulate=True)
+        return dx
     return gemm(dy, 0, W, 0, dx, M, K, N, epi, None, dgelu_aux, alpha, beta)
 
 

@@ -204,3 +204,35 @@ def test_persistent_walk_bit_identical(tmp_path):
         res[knob] = torch.load(path, weights_only=True)
     for k in res["0"]:
         assert torch.equal(res["0"][k], res["1"][k]), k
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("m,n,k", [(5000, 3072, 768),    # 256x256 persistent input-gradient walk, ragged M
+                                   (20992, 768, 3072),   # the text FFN2 -> dGELU shape
+                                   (2304, 1024, 3072),   # 256x128 / 128x128 tiles
+                                   (700, 300, 200)])     # small tiles, ragged everything
+def test_dgelu_colsum_slabs(dev, dtype, m, n, k):
+    """K3M_GEMM_COLSUM_SLABS: the dGELU input gradient also leaves the column sums of its output as 32-row
+    slabs (the bias gradient of the Linear it feeds): their sum equals the column sums of the stored C."""
+    from k3m_amd import ops, _lib as L
+    tdt = torch.float32 if dtype == "fp32" else torch.bfloat16
+    g = torch.Generator(device="cpu").manual_seed(m + n + k)
+    dy = torch.randn(m, k, generator=g).to(dev).to(tdt)
+    W = (torch.randn(k, n, generator=g) * 0.05).to(dev).to(tdt)
+    aux = torch.randn(m, n, generator=g).to(dev).to(tdt)
+    ns = (m + 31) // 32
+    ws = torch.full((ns * n,), float("nan"), device=dev)
+    c = torch.empty(m, n, device=dev, dtype=tdt)
+    ops.gemm(dy, 0, W, 0, c, m, n, k, L.EPI_DGELU | L.GEMM_COLSUM_SLABS, None, aux, 1.0, 0.0, 1, ws)
+    c_ref = torch.empty(m, n, device=dev, dtype=tdt)
+    ops.gemm(dy, 0, W, 0, c_ref, m, n, k, L.EPI_DGELU, None, aux, 1.0, 0.0)
+    torch.cuda.synchronize()
+    assert torch.equal(c, c_ref)                       # the flag does not change C
+    slabs = ws.view(ns, n)
+    assert torch.isfinite(slabs).all()                 # every slab row written, including the ragged last one
+    ref = c.double().sum(0)
+    got = slabs.double().sum(0)
+    assert float((got - ref).abs().max()) <= 1e-5 * float(ref.abs().max()) + 1e-6
+    # per 32-row group
+    grp = torch.nn.functional.pad(c.double(), (0, 0, 0, ns * 32 - m)).view(ns, 32, n).sum(1)
+    assert float((slabs.double() - grp).abs().max()) <= 1e-5 * float(grp.abs().max()) + 1e-6
