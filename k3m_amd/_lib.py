@@ -28,12 +28,13 @@ class K3mGemm(C.Structure):
     _fields_ = [("m", i32), ("n", i32), ("k", i32), ("a_trans", i32), ("b_trans", i32), ("epilogue", i32),
                 ("dtype", i32), ("splitk", i32), ("c_dtype", i32), ("lda", i64), ("ldb", i64), ("ldc", i64), ("ldaux", i64),
                 ("a", vp), ("b", vp), ("c", vp), ("bias", vp), ("aux", vp), ("ws", vp), ("alpha", f32),
-                ("beta", f32), ("f32_algo", i32)]
+                ("beta", f32), ("f32_algo", i32), ("a_planes", i64), ("b_planes", i64)]
 
 
 # name -> argtypes (restype is always int status)
 SIGNATURES = {
     "k3m_gemm": [C.POINTER(K3mGemm), vp],
+    "k3m_split3": [vp, i64, i32, i32, vp, i64, i64, vp],
     "k3m_colsum": [vp, i64, i32, i32, vp, i32, vp, i32, vp],
     "k3m_ln_fwd": [vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, f32, u64, u64, u64, i32, vp],
     "k3m_ln_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, u64, u64, u64, i32, vp, i32, vp],
