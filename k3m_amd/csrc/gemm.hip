@@ -133,6 +133,10 @@ bool prefer_256x256(const K3mGemm& g) {
 // Persistent x6 walk (gemm_x6p.hip) for the 256-row tiles: K3M_X6_PERSIST=0 restores one workgroup per
 // tile (A/B knob).
 const int kPersist = k3m_env_int("K3M_X6_PERSIST", 1);
+// fewest 256x128 tiles for the persistent 256-row walk (smaller grids take 128x128 / 64x64 tiles): 100 instead of
+// 200 moves the 2,304-2,368-row co-attention GEMMs off one-workgroup-per-CU 128x128 tiles, fp32 step +0.4-1.1 %
+// (profiles/r3_ab_x6_pmin.txt; A/B knob K3M_X6_P_MIN)
+const int kPersistMin = k3m_env_int("K3M_X6_P_MIN", 100);
 
 int cu_count() {
   static int n = [] {
@@ -209,7 +213,7 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
     const int vrc = kVariant ? k3m_x6_variant_launch(g, kVariant, st) : -1;
     if (vrc >= 0) {
       rc = vrc;
-    } else if (g.splitk > 1 || nblocks(g, 256, 128) >= 200) {
+    } else if (g.splitk > 1 || nblocks(g, 256, 128) >= kPersistMin) {
       if (kPersist) {
         rc = launch_x6_persistent_one(g, (ak || !bk) && prefer_256x256(g), ak, bk, st);
       } else if ((ak || !bk) && prefer_256x256(g)) {

@@ -271,6 +271,211 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   }
 }
 
+// ------------------------------------------------------------------ bf16 LayerNorm: half-wave rows, 16-B vectors
+// The bf16 forms of the two kernels above.  With one wave per row and 8-B (4 x bf16) vectors, a bf16 row
+// of 768 is three 512-B wave loads per operand and the kernels ran latency-bound at ~0.4 of the HBM
+// roofline (config-3 step: 108 + 108 launches, 10 % of the step).  Here a row is a HALF wave and every
+// access is a 16-B vector (8 bf16 per lane-chunk, cols/256 chunks per lane): twice the rows and the same
+// bytes in flight per wave with half the load instructions.  Same arithmetic, dropout counters and slab
+// layout as ln_fwd_kernel / ln_bwd_kernel (the row sums reduce in a different order).
+constexpr int MAXV8 = 4;   // 16-B chunks per lane: cols <= 32 * 8 * 4 = 1024
+
+__device__ __forceinline__ void ld8bf(const bf16_t* p, float (&v)[8]) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[2 * q] = __uint_as_float(w[q] << 16);
+    v[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void st8bf(bf16_t* p, const float (&v)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) w[q] = (uint32_t)from_f<bf16_t>(v[2 * q]).x | ((uint32_t)from_f<bf16_t>(v[2 * q + 1]).x << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
+  const floatx4 a = *reinterpret_cast<const floatx4*>(p), b = *reinterpret_cast<const floatx4*>(p + 4);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[q] = a[q];
+    v[4 + q] = b[q];
+  }
+}
+__device__ __forceinline__ float half_sum(float v) {   // over the 32 lanes of a half wave
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                          bf16_t* __restrict__ y, bf16_t* __restrict__ xhat,
+                                                          float* __restrict__ rstd, int rows, int cols, float eps,
+                                                          float p_in, float p_out, uint64_t seed, uint64_t off_in,
+                                                          uint64_t off_out) {
+  const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int l = threadIdx.x & 31;
+  if (row >= rows) return;   // half-wave uniform; the shuffles below stay inside the half
+  const int nv = cols >> 8;
+  const long long base = (long long)row * cols;
+  const K3mDrop din = k3m_drop_init(seed, p_in), dout = k3m_drop_init(seed, p_out);
+  float v[MAXV8][8];
+#pragma unroll
+  for (int j = 0; j < MAXV8; ++j)
+    if (j < nv) ld8bf(x + base + (l + 32 * j) * 8, v[j]);
+  float rv[MAXV8][8];
+  if (res) {
+#pragma unroll
+    for (int j = 0; j < MAXV8; ++j)
+      if (j < nv) ld8bf(res + base + (l + 32 * j) * 8, rv[j]);
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV8; ++j)
+    if (j < nv) {
+      const int c = (l + 32 * j) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float a = v[j][e];
+        if (p_in > 0.f) a *= k3m_drop(din, off_in + base + c + e);
+        if (res) a += rv[j][e];
+        v[j][e] = a;
+        sum += a;
+      }
+    }
+  const float mean = half_sum(sum) / cols;
+  float sq = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV8; ++j)
+    if (j < nv) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[j][e] -= mean;
+        sq += v[j][e] * v[j][e];
+      }
+    }
+  const float var = half_sum(sq) / cols;
+  const float rs = 1.0f / sqrtf(var + eps);
+  if (l == 0 && rstd) rstd[row] = rs;
+#pragma unroll
+  for (int j = 0; j < MAXV8; ++j)
+    if (j < nv) {
+      const int c = (l + 32 * j) * 8;
+      float xh[8], g[8], b[8], o[8];
+      ld8f(gamma + c, g);
+      ld8f(beta + c, b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        xh[e] = v[j][e] * rs;
+        o[e] = g[e] * xh[e] + b[e];
+        if (p_out > 0.f) o[e] *= k3m_drop(dout, off_out + base + c + e);
+      }
+      if (xhat) st8bf(xhat + base + c, xh);
+      st8bf(y + base + c, o);
+    }
+}
+
+__global__ __launch_bounds__(256) void ln_bwd_bf16_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ xhat,
+                                                          const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                                          bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
+                                                          float* __restrict__ ws, int rows, int cols, float p_in,
+                                                          float p_out, uint64_t seed, uint64_t off_in, uint64_t off_out,
+                                                          int acc_res, int want_sum) {
+  __shared__ float red[4][1024];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, l = lane & 31;
+  const int nv = cols >> 8;
+  const K3mDrop din = k3m_drop_init(seed, p_in), dout = k3m_drop_init(seed, p_out);
+  float pg[MAXV8][8], pb[MAXV8][8], px[MAXV8][8];
+#pragma unroll
+  for (int j = 0; j < MAXV8; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pg[j][e] = pb[j][e] = px[j][e] = 0.f;
+  // eight half-wave rows per block step (one row per half wave and step: two rows per wave in flight, as
+  // the one-wave-per-row kernel's two-row steps, at half its registers for the loads)
+  const int S = gridDim.x * 8;
+  for (int row = blockIdx.x * 8 + (threadIdx.x >> 5); row < rows; row += S) {
+    const long long base = (long long)row * cols;
+    float d[MAXV8][8], xv[MAXV8][8];
+#pragma unroll
+    for (int j = 0; j < MAXV8; ++j)
+      if (j < nv) {
+        ld8bf(dy + base + (l + 32 * j) * 8, d[j]);
+        ld8bf(xhat + base + (l + 32 * j) * 8, xv[j]);
+      }
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXV8; ++j)
+      if (j < nv) {
+        const int c = (l + 32 * j) * 8;
+        float g[8];
+        ld8f(gamma + c, g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float dd = d[j][e];
+          if (p_out > 0.f) dd *= k3m_drop(dout, off_out + base + c + e);
+          d[j][e] = dd;
+          pg[j][e] += dd * xv[j][e];
+          pb[j][e] += dd;
+          const float dxh = dd * g[e];
+          s1 += dxh;
+          s2 += dxh * xv[j][e];
+        }
+      }
+    const float m1 = half_sum(s1) / cols, m2 = half_sum(s2) / cols;
+    const float rs = rstd[row];
+#pragma unroll
+    for (int j = 0; j < MAXV8; ++j)
+      if (j < nv) {
+        const int c = (l + 32 * j) * 8;
+        float g[8], ds[8], dr[8];
+        ld8f(gamma + c, g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ds[e] = (d[j][e] * g[e] - m1 - xv[j][e] * m2) * rs;
+        if (acc_res) {
+          float old[8];
+          ld8bf(dres + base + c, old);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dr[e] = ds[e] + old[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dr[e] = ds[e];
+        }
+        st8bf(dres + base + c, dr);
+        if (dx != dres) {
+          if (p_in > 0.f) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) ds[e] *= k3m_drop(din, off_in + base + c + e);
+          }
+          st8bf(dx + base + c, ds);
+        }
+        if (want_sum) {   // the sum of dx as stored (bf16-rounded)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) px[j][e] += to_f(from_f<bf16_t>(ds[e]));
+        }
+      }
+  }
+  // the two half waves hold the same columns: fold them, then the 4 waves through LDS
+  for (int k = 0; k < (want_sum ? 3 : 2); ++k) {
+#pragma unroll
+    for (int j = 0; j < MAXV8; ++j)
+      if (j < nv) {
+        const int c = (l + 32 * j) * 8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float v = k == 0 ? pg[j][e] : (k == 1 ? pb[j][e] : px[j][e]);
+          v += __shfl_xor(v, 32, 64);
+          if (lane < 32) red[w][c + e] = v;
+        }
+      }
+    __syncthreads();
+    for (int c = threadIdx.x; c < cols; c += 256)
+      ws[((long long)k * gridDim.x + blockIdx.x) * cols + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------------ embeddings
 template <typename T>
 __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ ids, const int64_t* __restrict__ tt,
@@ -479,6 +684,13 @@ __global__ void scatter_add_rows_kernel(const T* src, long long lds, const int32
 
 int grid_for(long long n) { return (int)std::min<long long>((n + 255) / 256, 4096); }
 
+// The half-wave bf16 kernels win on long LayerNorms only (scripts/ln_bench.py, profiles/r3_ln_bf16.txt): forward
+// 32.0 -> 27.5 us at 20,992 x 768 and 14.9 -> 12.7 at 8,192, backward 53.5 -> 47.7 at 20,992, while the short
+// ones (2,304 rows) are 5-20 % slower.  A/B knob: K3M_LN_BF16_VEC=0 keeps every bf16 LayerNorm on the
+// one-wave-per-row kernels.
+const bool kLnBf16Vec = k3m_env_flag("K3M_LN_BF16_VEC", true);
+constexpr int LN_VEC_FWD_ROWS = 4096, LN_VEC_BWD_ROWS = 16384;
+
 }  // namespace
 
 #define DISPATCH_T(dtype, ...)            \
@@ -497,14 +709,26 @@ extern "C" int k3m_ln_fwd(const void* x, const void* res, const float* gamma, co
                           uint64_t off_in, uint64_t off_out, int dtype, hipStream_t st) {
   K3M_ARG(x && gamma && beta && y && rows >= 0 && cols % 256 == 0 && cols <= 1024 && cols > 0);
   if (rows == 0) return 0;
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ln_fwd_kernel<T>, dim3(k3m_cdiv(rows, 4)), dim3(256), 0, st,
-                                       (const T*)x, (const T*)res, gamma, beta, (T*)y, (T*)xhat, rstd, rows, cols, eps,
-                                       p_in, p_out, seed, off_in, off_out));
+  if (dtype == K3M_BF16 && kLnBf16Vec && rows >= LN_VEC_FWD_ROWS) {
+    hipLaunchKernelGGL(ln_fwd_bf16_kernel, dim3(k3m_cdiv(rows, 8)), dim3(256), 0, st, (const bf16_t*)x,
+                       (const bf16_t*)res, gamma, beta, (bf16_t*)y, (bf16_t*)xhat, rstd, rows, cols, eps, p_in, p_out,
+                       seed, off_in, off_out);
+  } else {
+    DISPATCH_T(dtype, hipLaunchKernelGGL(ln_fwd_kernel<T>, dim3(k3m_cdiv(rows, 4)), dim3(256), 0, st,
+                                         (const T*)x, (const T*)res, gamma, beta, (T*)y, (T*)xhat, rstd, rows, cols, eps,
+                                         p_in, p_out, seed, off_in, off_out));
+  }
   K3M_CHECK_LAUNCH();
   return 0;
 }
 
-static int ln_bwd_slab_count(int rows) { return std::max(1, std::min(LN_BWD_BLOCKS, k3m_cdiv(rows, 4))); }
+// at least kLnRowsPerSlab rows per slab (per workgroup): at 4, a short LayerNorm (2,304 rows) wrote 512 x 3
+// slabs of cols fp32, more bytes than it reads; 8 measured 2,304 x 768 19.6 -> 17.1 us, 2,368 x 1,024 21.9 ->
+// 20.3 (backward + its reduction, fp32 and bf16 alike), no change on the long ones (profiles/r3_ln_bf16.txt)
+const int kLnRowsPerSlab = k3m_env_int("K3M_LN_ROWS_PER_SLAB", 8);
+static int ln_bwd_slab_count(int rows) {
+  return std::max(1, std::min(LN_BWD_BLOCKS, k3m_cdiv(rows, kLnRowsPerSlab)));
+}
 
 extern "C" int k3m_ln_bwd_nslab(int rows, int* nslab) {
   K3M_ARG(nslab && rows >= 0);
@@ -519,9 +743,15 @@ extern "C" int k3m_ln_bwd_slabs(const void* dy, const void* xhat, const float* r
   K3M_ARG(cols % 256 == 0 && cols <= 1024 && rows >= 0);
   if (rows == 0) return 0;
   const int nb = ln_bwd_slab_count(rows);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3(nb), dim3(256), 0, st, (const T*)dy, (const T*)xhat, rstd,
-                                       gamma, (T*)dres, (T*)dx, ws, rows, cols, p_in, p_out, seed, off_in, off_out,
-                                       acc_res, want_sum));
+  if (dtype == K3M_BF16 && kLnBf16Vec && rows >= LN_VEC_BWD_ROWS) {
+    hipLaunchKernelGGL(ln_bwd_bf16_kernel, dim3(nb), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)xhat, rstd,
+                       gamma, (bf16_t*)dres, (bf16_t*)dx, ws, rows, cols, p_in, p_out, seed, off_in, off_out, acc_res,
+                       want_sum);
+  } else {
+    DISPATCH_T(dtype, hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3(nb), dim3(256), 0, st, (const T*)dy, (const T*)xhat,
+                                         rstd, gamma, (T*)dres, (T*)dx, ws, rows, cols, p_in, p_out, seed, off_in,
+                                         off_out, acc_res, want_sum));
+  }
   K3M_CHECK_LAUNCH();
   return 0;
 }

@@ -99,12 +99,13 @@ def _ln_ref(s, g, b):
     return g * (s - u) / torch.sqrt(v + 1e-12) + b
 
 
-@pytest.mark.parametrize("cols", [768, 1024])
-def test_layernorm_bf16(dev, cols):
+@pytest.mark.parametrize("cols,M", [(768, 999), (1024, 999),
+                                    # the half-wave 16-B kernels (forward >= 4,096 rows, backward >= 16,384)
+                                    (768, 5000), (768, 16500), (1024, 16400)])
+def test_layernorm_bf16(dev, cols, M):
     """bf16 activations in/out, fp32 statistics and parameter gradients; reference = fp32 math on
     the bf16 inputs; tolerance = bf16 output rounding."""
     from k3m_amd import ops
-    M = 999
     x = torch.randn(M, cols, device=dev).bfloat16()
     r = torch.randn(M, cols, device=dev).bfloat16()
     g = 1 + 0.1 * torch.randn(cols, device=dev)
@@ -126,6 +127,36 @@ def test_layernorm_bf16(dev, cols):
     assert _rel(dres, xr.grad) < 2.0 ** -6
     assert _rel(dg, gr.grad) < 1e-2
     assert _rel(db, br.grad) < 1e-4
+
+
+@pytest.mark.parametrize("M", [999, 16500])
+def test_layernorm_bf16_dropout_acc(dev, M):
+    """bf16 LayerNorm with input dropout, an accumulated residual gradient and the fused dx column sums (the
+    engine's post-LN tail): the backward regenerates the forward's mask; matches the fp32 kernels run on the
+    same bf16 values within bf16 rounding."""
+    from k3m_amd import ops
+    cols = 768
+    x = torch.randn(M, cols, device=dev).bfloat16()
+    r = torch.randn(M, cols, device=dev).bfloat16()
+    g = 1 + 0.1 * torch.randn(cols, device=dev)
+    b = 0.1 * torch.randn(cols, device=dev)
+    dy = torch.randn(M, cols, device=dev).bfloat16()
+    acc0 = torch.randn(M, cols, device=dev).bfloat16()
+    out = {}
+    for dt in (torch.bfloat16, torch.float32):
+        xx, rr, dd = x.to(dt), r.to(dt), dy.to(dt)
+        y, xh = torch.empty_like(xx), torch.empty_like(xx)
+        rs = torch.empty(M, device=dev)
+        ops.ln_fwd(xx, rr, g, b, y, xh, rs, p_in=0.1, seed=9, off_in=123)
+        dres, dx = acc0.to(dt).clone(), torch.empty_like(xx)
+        dg, db, xs = (torch.zeros(cols, device=dev) for _ in range(3))
+        ops.ln_bwd(dd, xh.to(dt), rs, g, dres, dx, dg, db, p_in=0.1, seed=9, off_in=123, acc_res=True, dxsum=xs)
+        out[dt] = [t.float() for t in (y, dres, dx, dg, db, xs)]
+    for a, c in zip(out[torch.bfloat16][:3], out[torch.float32][:3]):
+        assert _rel(a, c) < 2.0 ** -6
+    assert torch.equal(out[torch.bfloat16][2] == 0, out[torch.float32][2] == 0)   # the same dropout mask
+    for a, c in zip(out[torch.bfloat16][3:], out[torch.float32][3:]):
+        assert _rel(a, c) < 2e-2
 
 
 def test_colsum_bf16(dev):
