@@ -498,8 +498,10 @@ int big_launch(const K3mGemm& g, hipStream_t st) {
             : big_launch_epi<TBM, TBN, WM, WN, true, false, bf16_t>(g, st);
 }
 
-// tile policy: 256x256 when it still gives >= ~3/4 of a wave of blocks, else 256x128
-bool big_prefers_256(long long nb256) { return nb256 >= 192; }
+// tile policy: 256x256 when it still gives >= 1/2 of a wave of blocks, else 256x128 (A/B knob K3M_B16_256;
+// 128 vs 192: bf16 step +0.35 %, 256: -4 %, profiles/r3_ab_b16_policy.txt)
+const int kB16Min256 = k3m_env_int("K3M_B16_256", 128);
+bool big_prefers_256(long long nb256) { return nb256 >= kB16Min256; }
 
 template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, typename CT, int MF>
 int big_grouped_epi_mf(const k3m_b16::GemmGroup& grp, int epi, hipStream_t st) {
@@ -564,6 +566,9 @@ bool vec_of(const K3mGemm& g) {
 
 // K3M_BF16_BIG=0 keeps every bf16 GEMM on the 128x128 register-staged kernel (A/B switch)
 const bool kBig = k3m_env_flag("K3M_BF16_BIG", true);
+// fewest 256x128 tiles for the large-tile kernel; smaller grids take the 128x128 / 64x128 kernel (A/B knob;
+// 80 vs 160: bf16 step +0.4-0.5 %, profiles/r3_ab_b16_policy.txt)
+const int kB16Min = k3m_env_int("K3M_B16_MIN", 80);
 
 }  // namespace
 
@@ -587,7 +592,7 @@ int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st, bool slabs_only, bool c
   int rc;
   const long long nb256 = nb_of(g, 256, 256), nb128 = nb_of(g, 256, 128);
   bool fused = false;   // the large-tile epilogue writes the COLSUM_SLABS itself
-  if (kBig && big_ok(g, vec) && nb128 >= 160) {
+  if (kBig && big_ok(g, vec) && nb128 >= kB16Min) {
     rc = big_prefers_256(nb256) ? big_launch<256, 256, 2, 4>(g, st) : big_launch<256, 128, 4, 2>(g, st);
     fused = true;
   } else {

@@ -241,6 +241,11 @@ def linear_dgrad(dy, W, dx=None, beta=0.0, dgelu_aux=None, alpha=1.0, colsum_out
     return gemm(dy, 0, W, 0, dx, M, K, N, epi, None, dgelu_aux, alpha, beta)
 
 
+# relative cost per extra split-K slice (its slab write + read), fp32 / bf16 weight gradients (A/B knobs)
+SPLITK_COST_F32 = float(os.environ.get("K3M_SPLITK_COST_F32", "0.01"))
+SPLITK_COST_BF16 = float(os.environ.get("K3M_SPLITK_COST_BF16", "0.02"))
+
+
 def _splitk(m, n, k, dtype=torch.float32):
     """K-split of a weight-gradient GEMM (C[m,n] summed over k ~ 20k rows): enough blocks to fill
     the 256 CUs in whole waves.  fp32 (bf16x6 kernel) tiles are 256x128 at one block per CU;
@@ -252,7 +257,7 @@ def _splitk(m, n, k, dtype=torch.float32):
         # minimise (waves of 256 blocks) x (k per split), plus ~1% per split for the slab reduction
         best, best_cost = 1, float("inf")
         for s in range(1, min(32, k // 1024) + 1):
-            cost = ((tiles * s + 255) // 256) / s * (1.0 + 0.01 * s)
+            cost = ((tiles * s + 255) // 256) / s * (1.0 + SPLITK_COST_F32 * s)
             if cost < best_cost - 1e-9:
                 best, best_cost = s, cost
         return best
@@ -263,7 +268,7 @@ def _splitk(m, n, k, dtype=torch.float32):
             return 1
         best, best_cost = 1, float("inf")
         for s in range(1, min(32, k // 1024) + 1):
-            cost = ((tiles * s + 255) // 256) / s * (1.0 + 0.02 * s)
+            cost = ((tiles * s + 255) // 256) / s * (1.0 + SPLITK_COST_BF16 * s)
             if cost < best_cost - 1e-9:
                 best, best_cost = s, cost
         return best
