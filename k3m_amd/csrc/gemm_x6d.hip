@@ -242,12 +242,134 @@ __device__ __forceinline__ void mainloop3(const K3mGemm& g, long long pa, long l
   __syncthreads();
 }
 
+// mainloop3 with the fragment reads of k-tile kt+1 interleaved with the MFMAs of kt (lab, K3M_X6D_VARIANT=2):
+// F(kt) is in registers when iteration kt starts; after its barrier (DMA of kt+1 landed everywhere, stage kt
+// free) the DMA of kt+3 goes to stage kt%3, the A fragments of kt+1 are read into spare registers, and each
+// column group j of MFMAs is followed by the reads of kt+1's B fragments j, whose registers it just freed.
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_>
+__device__ __forceinline__ void mainloop3p(const K3mGemm& g, long long pa, long long pb, int m0, int n0, int kbeg,
+                                           int kend, __bf16* img, floatx16 (&acc)[TBM / WM / 32][TBN / WN / 32]) {
+  constexpr int NT = 64 * WM * WN, FM = TBM / WM / 32, FN = TBN / WN / 32;
+  constexpr int STAGE = 3 * (TBM + TBN) * BK, PA = TBM * BK, PB = TBN * BK;
+  using LA = PLoader<AK, TBM, NT>;
+  using LB = PLoader<BK_, TBN, NT>;
+  constexpr int VMC = LA::NI + LB::NI;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
+  if (nk == 0) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = (w / WN) * (TBM / WM), wn = (w % WN) * (TBN / WN);
+  const int h = lane >> 5, cl = lane & 31;
+  auto rdA = [&](const __bf16* st, int pl, int i) {
+    return AK ? *reinterpret_cast<const bf16x8*>(st + pl * PA + slot_off<BK>(wm + 32 * i + cl, h))
+              : mn_frag<TBM>(st + pl * PA, wm + 32 * i, 0, lane);
+  };
+  auto rdB = [&](const __bf16* st, int pl, int j) {
+    const __bf16* bs = st + 3 * PA;
+    return BK_ ? *reinterpret_cast<const bf16x8*>(bs + pl * PB + slot_off<BK>(wn + 32 * j + cl, h))
+               : mn_frag<TBN>(bs + pl * PB, wn + 32 * j, 0, lane);
+  };
+  LA la;
+  LB lb;
+  la.init(static_cast<const uint16_t*>(g.a), g.lda, pa, m0, kbeg, g.m);
+  lb.init(static_cast<const uint16_t*>(g.b), g.ldb, pb, n0, kbeg, g.n);
+  la.issue(img);
+  lb.issue(img + 3 * PA);
+  if (nk > 1) {
+    la.issue(img + STAGE);
+    lb.issue(img + STAGE + 3 * PA);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if (nk > 2) {
+    la.issue(img + 2 * STAGE);
+    lb.issue(img + 2 * STAGE + 3 * PA);
+  }
+  bf16x8 a[3][FM], b[3][FN];
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) a[pl][i] = rdA(img, pl, i);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) b[pl][j] = rdB(img, pl, j);
+  }
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) {
+      if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 3 < nk) {
+      la.issue(img + cur * STAGE);
+      lb.issue(img + cur * STAGE + 3 * PA);
+    }
+    const int nx = cur == 2 ? 0 : cur + 1;
+    const __bf16* ns = img + nx * STAGE;   // stage of kt+1 (stale past the last tile: read, never used)
+    bf16x8 na[3][FM], nb[3][FN];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) na[pl][FM - 1] = rdA(ns, pl, FM - 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < FM - 1; ++i) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) na[pl][i] = rdA(ns, pl, i);   // row i's A fragments are dead
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    constexpr int I = FM - 1;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      acc[I][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][I], b[2][j], acc[I][j], 0, 0, 0);
+      acc[I][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][I], b[1][j], acc[I][j], 0, 0, 0);
+      acc[I][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][I], b[0][j], acc[I][j], 0, 0, 0);
+      acc[I][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][I], b[1][j], acc[I][j], 0, 0, 0);
+      acc[I][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][I], b[0][j], acc[I][j], 0, 0, 0);
+      acc[I][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][I], b[0][j], acc[I][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) nb[pl][j] = rdB(ns, pl, j);   // column j's B fragments are dead
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[pl][i] = na[pl][i];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[pl][j] = nb[pl][j];
+    }
+    cur = nx;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 // NST = 3: 256x256 / 8 waves / one workgroup per CU (mainloop3); NST = 2: 256x128 / 4 waves / two per CU
 template <int TBM, int TBN, int WM, int WN, int NST>
 struct Lds {
+  static constexpr int STAGES = NST == 4 ? 3 : NST;
   static constexpr int STAGE_F = 3 * (TBM + TBN) * BK / 2;   // floats per stage
   static constexpr int EPI_F = WM * WN * 32 * (TBN / WN + 8);
-  static constexpr int WORDS = NST * STAGE_F > EPI_F ? NST * STAGE_F : EPI_F;
+  static constexpr int WORDS = STAGES * STAGE_F > EPI_F ? STAGES * STAGE_F : EPI_F;
 };
 
 template <int TBM, int TBN, int WM, int WN, int NST, bool AK, bool BK_, int EPI>
@@ -263,7 +385,9 @@ __global__ __launch_bounds__(64 * WM * WN, NST == 2 ? 2 : 1) void gemm_x6d_kerne
     kend = min(g.k, kbeg + per);
   }
   floatx16 acc[TBM / WM / 32][TBN / WN / 32];
-  if constexpr (NST == 3)
+  if constexpr (NST == 4)   // lab: three stages with the fragment reads of kt+1 under the MFMAs of kt
+    mainloop3p<TBM, TBN, WM, WN, AK, BK_>(g, pa, pb, m0, n0, kbeg, kend, reinterpret_cast<__bf16*>(smem), acc);
+  else if constexpr (NST == 3)
     mainloop3<TBM, TBN, WM, WN, AK, BK_>(g, pa, pb, m0, n0, kbeg, kend, reinterpret_cast<__bf16*>(smem), acc);
   else
     mainloop2<TBM, TBN, WM, WN, AK, BK_>(g, pa, pb, m0, n0, kbeg, kend, reinterpret_cast<__bf16*>(smem), acc);
@@ -317,7 +441,8 @@ __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ x
 
 namespace {
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
-const int kX6dVariant = k3m_env_int("K3M_X6D_VARIANT", 0);   // lab knob: 0 = 256x256 three stages, 1 = 256x128 x2
+// lab knob: 0 = 256x256 three stages, 1 = 256x128 two workgroups per CU, 2 = variant 0 with pipelined fragment reads
+const int kX6dVariant = k3m_env_int("K3M_X6D_VARIANT", 0);
 }  // namespace
 
 extern "C" int k3m_split3(const float* x, long long ldx, int rows, int cols, void* planes, long long ldp,
@@ -346,6 +471,12 @@ int k3m_gemm_x6d_impl(const K3mGemm& g, long long pa, long long pb, hipStream_t 
   K3M_ARG((long long)(ak ? g.m : g.k) * (ak ? g.lda : g.lda) < (1LL << 32));
   K3M_ARG((long long)(bk ? g.n : g.k) * g.ldb < (1LL << 32));
   using namespace k3m_x6d;
+  if (kX6dVariant == 2) {   // lab: 256x256, three stages, fragment reads of kt+1 under the MFMAs of kt
+    if (ak && bk) return launch<256, 256, 4, 2, 4, true, true>(g, pa, pb, st);
+    if (ak) return launch<256, 256, 2, 4, 4, true, false>(g, pa, pb, st);
+    if (!bk) return launch<256, 256, 2, 4, 4, false, false>(g, pa, pb, st);
+    return launch<256, 256, 2, 4, 4, false, true>(g, pa, pb, st);
+  }
   if (kX6dVariant == 1) {   // 256x128, two workgroups per CU
     if (ak && bk) return launch<256, 128, 2, 2, 2, true, true>(g, pa, pb, st);
     if (ak) return launch<256, 128, 2, 2, 2, true, false>(g, pa, pb, st);
