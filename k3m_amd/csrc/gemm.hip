@@ -137,6 +137,9 @@ const int kPersist = k3m_env_int("K3M_X6_PERSIST", 1);
 // 200 moves the 2,304-2,368-row co-attention GEMMs off one-workgroup-per-CU 128x128 tiles, fp32 step +0.4-1.1 %
 // (profiles/r3_ab_x6_pmin.txt; A/B knob K3M_X6_P_MIN)
 const int kPersistMin = k3m_env_int("K3M_X6_P_MIN", 100);
+// fewest 128x128 tiles for the 128x128 x6 kernel; smaller grids take 64x64 tiles (A/B knob; 50 measured equal,
+// profiles/r3_ab_knobs_recheck.txt)
+const int kT128Min = k3m_env_int("K3M_X6_T128_MIN", 200);
 
 int cu_count() {
   static int n = [] {
@@ -227,7 +230,7 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
         rc = launch_x6<256, 128, 4, 2, 32, 1>(g, ak, bk, st);
       }
     }
-    else if (nblocks(g, 128, 128) >= 200) rc = launch_x6<128, 128, 2, 2, 32, 1>(g, ak, bk, st);
+    else if (nblocks(g, 128, 128) >= kT128Min) rc = launch_x6<128, 128, 2, 2, 32, 1>(g, ak, bk, st);
     // 64x64 runs at BK = 16: the BK = 32 build of this tile (ROCm 7.2 hipcc) returned C = alpha*AB
     // without the beta*C term for scattered 16-lane groups (scripts/lab/gemm_dbg.hip reproduces it;
     // tests/test_gpu_gemm_x6.py::test_x6_beta_all_tiles guards every tile path)
