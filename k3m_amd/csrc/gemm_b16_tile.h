@@ -622,4 +622,27 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_grouped_kernel(GemmGroup
   run_tile<TBM, TBN, WM, WN, AK, BK_, EPI, CT, MF>(g, m0, n0, kbeg, kend, slice, smem);
 }
 
+// Persistent walk (K3M_B16_PERSIST): min(units, CUs) workgroups, each running units u, u + gridDim.x, ...
+// of the group (problem, split slice, tile), the units of one "wave" (u / gridDim.x) remapped XCD-aware as in
+// the one-unit-per-workgroup grid.  Same tiles, same arithmetic: bit-identical C; the LDS stages are free
+// between units (every epilogue ends on a barrier).
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF>
+__global__ __launch_bounds__(64 * WM * WN, 1) void gemm_persist_kernel(GemmGroup grp) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[Shape<TBM, TBN, WM, WN>::LDS];
+  const int total = grp.start[grp.count];
+  const int P = gridDim.x;
+  for (int u = blockIdx.x; u < total; u += P) {   // uniform over the workgroup: every wave leaves together
+    const int base = (u / P) * P, cnt = min(P, total - base);
+    const int id = base + xcd_remap(u - base, cnt);
+    int p = 0;
+    while (p + 1 < grp.count && id >= grp.start[p + 1]) ++p;
+    p = __builtin_amdgcn_readfirstlane(p);
+    const K3mGemm& g = grp.g[p];
+    int m0, n0, slice, kbeg, kend;
+    coords(id - grp.start[p], g.m, g.n, TBM, TBN, m0, n0, slice);
+    k_range(g, slice, kbeg, kend);
+    run_tile<TBM, TBN, WM, WN, AK, BK_, EPI, CT, MF>(g, m0, n0, kbeg, kend, slice, smem);
+  }
+}
+
 }  // namespace k3m_b16

@@ -457,13 +457,49 @@ long long nb_of(const K3mGemm& g, int bm, int bn) {
 const int kMF = k3m_env_int("K3M_B16_MF", 0);
 inline bool use_mf32(bool bk) { return kMF == 32 || (kMF != 16 && !bk); }
 
+// The large-tile GEMMs as a persistent walk of min(units, CUs) workgroups (gemm_persist_kernel): bit-identical,
+// bf16 step +0.4 % in three interleaved pairs (profiles/r3_ab_b16_persist.txt); K3M_B16_PERSIST=0 launches one
+// workgroup per tile (A/B knob)
+const bool kB16Persist = k3m_env_flag("K3M_B16_PERSIST", true);
+int b16_cus() {
+  static int n = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      return 256;
+    return cus;
+  }();
+  return n;
+}
+
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF>
+void persist_launch(const k3m_b16::GemmGroup& grp, hipStream_t st) {
+  const int total = grp.start[grp.count];
+  const int nblk = total < b16_cus() ? total : b16_cus();
+  hipLaunchKernelGGL((k3m_b16::gemm_persist_kernel<TBM, TBN, WM, WN, AK, BK_, EPI, CT, MF>), dim3(nblk),
+                     dim3(64 * WM * WN), 0, st, grp);
+}
+
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF>
+void one_launch(const K3mGemm& g, hipStream_t st) {
+  if (kB16Persist) {
+    k3m_b16::GemmGroup grp = {};
+    grp.g[0] = g;
+    grp.start[0] = 0;
+    grp.start[1] = (int)nb_of(g, TBM, TBN);
+    grp.count = 1;
+    persist_launch<TBM, TBN, WM, WN, AK, BK_, EPI, CT, MF>(grp, st);
+    return;
+  }
+  hipLaunchKernelGGL((k3m_b16::gemm_kernel<TBM, TBN, WM, WN, AK, BK_, EPI, CT, MF>), dim3((unsigned)nb_of(g, TBM, TBN)),
+                     dim3(64 * WM * WN), 0, st, g);
+}
+
 template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, typename CT, int MF>
 int big_launch_epi_mf(const K3mGemm& g, hipStream_t st) {
-  const dim3 grid((unsigned)nb_of(g, TBM, TBN));
   switch (g.epilogue) {
 #define K3M_GEMM_CASE(E)                                                                                     \
     case E:                                                                                                  \
-      hipLaunchKernelGGL((k3m_b16::gemm_kernel<TBM, TBN, WM, WN, AK, BK_, E, CT, MF>), grid, dim3(64 * WM * WN), 0, st, g); \
+      one_launch<TBM, TBN, WM, WN, AK, BK_, E, CT, MF>(g, st);                                               \
       break;
     K3M_GEMM_CASE(K3M_EPI_NONE)
     K3M_GEMM_CASE(K3M_EPI_BIAS)
@@ -487,8 +523,7 @@ int big_launch(const K3mGemm& g, hipStream_t st) {
   const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
   if (!ak) {
     if (g.epilogue != K3M_EPI_NONE) return K3M_EINVAL;
-    hipLaunchKernelGGL((k3m_b16::gemm_kernel<TBM, TBN, WM, WN, false, false, K3M_EPI_NONE, float, 32>),
-                       dim3((unsigned)nb_of(g, TBM, TBN)), dim3(64 * WM * WN), 0, st, g);
+    one_launch<TBM, TBN, WM, WN, false, false, K3M_EPI_NONE, float, 32>(g, st);
     return 0;
   }
   if (g.c_dtype == K3M_F32)
@@ -509,8 +544,11 @@ int big_grouped_epi_mf(const k3m_b16::GemmGroup& grp, int epi, hipStream_t st) {
   switch (epi) {
 #define K3M_GROUP_CASE(E)                                                                                      \
     case E:                                                                                                    \
-      hipLaunchKernelGGL((k3m_b16::gemm_grouped_kernel<TBM, TBN, WM, WN, AK, BK_, E, CT, MF>), grid, dim3(64 * WM * WN), \
-                         0, st, grp);                                                                          \
+      if (kB16Persist)                                                                                         \
+        persist_launch<TBM, TBN, WM, WN, AK, BK_, E, CT, MF>(grp, st);                                         \
+      else                                                                                                     \
+        hipLaunchKernelGGL((k3m_b16::gemm_grouped_kernel<TBM, TBN, WM, WN, AK, BK_, E, CT, MF>), grid,         \
+                           dim3(64 * WM * WN), 0, st, grp);                                                    \
       break;
     K3M_GROUP_CASE(K3M_EPI_NONE)
     K3M_GROUP_CASE(K3M_EPI_BIAS)
@@ -535,8 +573,11 @@ int big_grouped(const k3m_b16::GemmGroup& grp, hipStream_t st) {
   const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
   if (!ak) {
     if (g.epilogue != K3M_EPI_NONE) return K3M_EINVAL;
-    hipLaunchKernelGGL((k3m_b16::gemm_grouped_kernel<TBM, TBN, WM, WN, false, false, K3M_EPI_NONE, float, 32>),
-                       dim3(grp.start[grp.count]), dim3(64 * WM * WN), 0, st, grp);
+    if (kB16Persist)
+      persist_launch<TBM, TBN, WM, WN, false, false, K3M_EPI_NONE, float, 32>(grp, st);
+    else
+      hipLaunchKernelGGL((k3m_b16::gemm_grouped_kernel<TBM, TBN, WM, WN, false, false, K3M_EPI_NONE, float, 32>),
+                         dim3(grp.start[grp.count]), dim3(64 * WM * WN), 0, st, grp);
     return 0;
   }
   if (g.c_dtype == K3M_F32)
