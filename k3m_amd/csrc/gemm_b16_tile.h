@@ -189,7 +189,7 @@ __device__ __forceinline__ void mfmas(floatx4 (&acc)[FM][FN], const bf16x8 (&a)[
 template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_>
 __device__ __forceinline__ void mainloop(const uint16_t* __restrict__ A, long long lda, const uint16_t* __restrict__ B,
                                          long long ldb, int M, int N, int m0, int n0, int kbeg, int kend,
-                                         uint16_t* smem, Acc<16, TBM / WM, TBN / WN>& accs) {
+                                         uint16_t* smem, Acc<16, TBM / WM, TBN / WN>& accs, bool pre = false) {
   using S = Shape<TBM, TBN, WM, WN>;
   constexpr int FM = S::FM, FN = S::FN;
   auto& acc = accs.v;
@@ -205,8 +205,13 @@ __device__ __forceinline__ void mainloop(const uint16_t* __restrict__ A, long lo
   lb.init(B, ldb, n0, kbeg, N);
   const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
   if (nk == 0) return;
-  la.issue(smem);
-  lb.issue(smem + TBM * BK);
+  if (pre) {   // k-tile 0 already in flight to stage 0 (issued by the previous tile's epilogue)
+    la.base += la.step;
+    lb.base += lb.step;
+  } else {
+    la.issue(smem);
+    lb.issue(smem + TBM * BK);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (nk > 1) {
@@ -248,7 +253,7 @@ template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_>
 __device__ __forceinline__ void mainloop32(const uint16_t* __restrict__ A, long long lda,
                                            const uint16_t* __restrict__ B, long long ldb, int M, int N, int m0,
                                            int n0, int kbeg, int kend, uint16_t* smem,
-                                           Acc<32, TBM / WM, TBN / WN>& accs) {
+                                           Acc<32, TBM / WM, TBN / WN>& accs, bool pre = false) {
   using S = Shape<TBM, TBN, WM, WN>;
   constexpr int FM = TBM / WM / 32, FN = TBN / WN / 32;
   auto& acc = accs.v;
@@ -266,8 +271,13 @@ __device__ __forceinline__ void mainloop32(const uint16_t* __restrict__ A, long 
   lb.init(B, ldb, n0, kbeg, N);
   const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
   if (nk == 0) return;
-  la.issue(smem);
-  lb.issue(smem + TBM * BK);
+  if (pre) {   // k-tile 0 already in flight to stage 0 (issued by the previous tile's epilogue)
+    la.base += la.step;
+    lb.base += lb.step;
+  } else {
+    la.issue(smem);
+    lb.issue(smem + TBM * BK);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (nk > 1) {
@@ -399,12 +409,17 @@ __device__ __forceinline__ void epi_math8(const float (&v)[8], const float (&bb)
 // falling back to vmcnt(0) (which had drained every store of a pass before the next one).  Edge tiles
 // keep the guarded per-element path.
 // 16x16 accumulator layout: acc[i][j][r] = C[wm + 16 i + 4 (lane >> 4) + r][wn + 16 j + (lane & 15)].
-template <int TBM, int TBN, int WM, int WN, int EPI, typename CT, typename AccT>
+struct NoHookB {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+// hook(): called once, after the first accumulator group is in LDS and before any global store of C (the
+// persistent walk issues the next tile's first LDS-DMA there; the staging image then must not overlap stage 0).
+template <int TBM, int TBN, int WM, int WN, int EPI, typename CT, typename AccT, class Hook = NoHookB>
 __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint16_t* smem_u16, const AccT& acc,
-                                         int slice) {
+                                         int slice, Hook hook = Hook()) {
   using S = Shape<TBM, TBN, WM, WN>;
   constexpr int WNC = TBN / WN, WS = WNC + 8, LPR = WNC / 8, RPP = 64 / LPR, NPS = 32 / RPP, NG = TBM / WM / 32;
-  static_assert(S::NT / 64 * 32 * WS * 4 <= S::LDS * 2, "epilogue staging exceeds the LDS stages");
   constexpr int RING = sizeof(CT) == 2 ? 2 : 1;   // passes the per-pass loads run ahead (register budget)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = (w / WN) * (TBM / WM), wn = (w % WN) * WNC;
@@ -460,6 +475,7 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint1
       for (int grp = 0; grp < NG; ++grp) {
         acc.stage(grp, wl, WS, lane);
         __syncthreads();
+        if (grp == 0) hook();
 #pragma unroll
         for (int ps = 0; ps < NPS; ++ps) {
           const int q = grp * NPS + ps, slot = q % RING;
@@ -497,6 +513,7 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint1
   for (int grp = 0; grp < NG; ++grp) {
     acc.stage(grp, wl, WS, lane);
     __syncthreads();
+    if (grp == 0) hook();
 #pragma unroll 1
     for (int ps = 0; ps < NPS; ++ps) {
       const int rr = ps * RPP + lr;
@@ -582,9 +599,15 @@ struct GemmGroup {
 };
 
 // one output tile on MF x MF x (512 / MF) MFMAs (MF = 16 or 32)
+template <int TBM, int TBN, int WM, int WN>
+struct EpiLds {   // bf16 elements of the epilogue's fp32 staging image (8 waves x 32 rows x (TBN/WN + 8))
+  static constexpr int E = Shape<TBM, TBN, WM, WN>::NT / 64 * 32 * (TBN / WN + 8) * 2;
+};
+
 template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF>
 __device__ __forceinline__ void run_tile(const K3mGemm& g, int m0, int n0, int kbeg, int kend, int slice,
                                          uint16_t* smem) {
+  static_assert(EpiLds<TBM, TBN, WM, WN>::E <= Shape<TBM, TBN, WM, WN>::LDS, "epilogue staging exceeds the LDS stages");
   Acc<MF, TBM / WM, TBN / WN> acc;
   if constexpr (MF == 32)
     mainloop32<TBM, TBN, WM, WN, AK, BK_>(static_cast<const uint16_t*>(g.a), g.lda, static_cast<const uint16_t*>(g.b),
@@ -624,24 +647,74 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_grouped_kernel(GemmGroup
 
 // Persistent walk (K3M_B16_PERSIST): min(units, CUs) workgroups, each running units u, u + gridDim.x, ...
 // of the group (problem, split slice, tile), the units of one "wave" (u / gridDim.x) remapped XCD-aware as in
-// the one-unit-per-workgroup grid.  Same tiles, same arithmetic: bit-identical C; the LDS stages are free
-// between units (every epilogue ends on a barrier).
-template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF>
-__global__ __launch_bounds__(64 * WM * WN, 1) void gemm_persist_kernel(GemmGroup grp) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[Shape<TBM, TBN, WM, WN>::LDS];
-  const int total = grp.start[grp.count];
-  const int P = gridDim.x;
-  for (int u = blockIdx.x; u < total; u += P) {   // uniform over the workgroup: every wave leaves together
+// the one-unit-per-workgroup grid.  Same tiles, same arithmetic: bit-identical C.  PRE (K3M_B16_PREFETCH): the
+// epilogue stages through an image placed after stage 0, and issues the next unit's first k-tile of LDS-DMA
+// into stage 0 before its first store, so that load overlaps this tile's epilogue.
+template <int TBM, int TBN, int WM, int WN>
+struct PUnit {
+  int p, m0, n0, slice, kbeg, kend;
+  __device__ __forceinline__ void decode(const GemmGroup& grp, int u) {
+    const int total = grp.start[grp.count];
+    const int P = gridDim.x;
     const int base = (u / P) * P, cnt = min(P, total - base);
     const int id = base + xcd_remap(u - base, cnt);
-    int p = 0;
+    p = 0;
     while (p + 1 < grp.count && id >= grp.start[p + 1]) ++p;
     p = __builtin_amdgcn_readfirstlane(p);
     const K3mGemm& g = grp.g[p];
-    int m0, n0, slice, kbeg, kend;
     coords(id - grp.start[p], g.m, g.n, TBM, TBN, m0, n0, slice);
     k_range(g, slice, kbeg, kend);
-    run_tile<TBM, TBN, WM, WN, AK, BK_, EPI, CT, MF>(g, m0, n0, kbeg, kend, slice, smem);
+  }
+};
+
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF, bool PRE>
+__global__ __launch_bounds__(64 * WM * WN, 1) void gemm_persist_kernel(GemmGroup grp) {
+  using S = Shape<TBM, TBN, WM, WN>;
+  constexpr int EOFF = PRE ? TBM * BK + TBN * BK : 0;   // the epilogue image after stage 0 when prefetching
+  constexpr int WORDS = (EOFF + EpiLds<TBM, TBN, WM, WN>::E > S::LDS) ? EOFF + EpiLds<TBM, TBN, WM, WN>::E : S::LDS;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[WORDS];
+  const int total = grp.start[grp.count];
+  int u = blockIdx.x;
+  if (u >= total) return;
+  PUnit<TBM, TBN, WM, WN> cur;
+  cur.decode(grp, u);
+  bool pre = false;
+  for (;;) {   // uniform over the workgroup: every wave leaves together
+    const K3mGemm& g = grp.g[cur.p];
+    Acc<MF, TBM / WM, TBN / WN> acc;
+    if constexpr (MF == 32)
+      mainloop32<TBM, TBN, WM, WN, AK, BK_>(static_cast<const uint16_t*>(g.a), g.lda, static_cast<const uint16_t*>(g.b),
+                                            g.ldb, g.m, g.n, cur.m0, cur.n0, cur.kbeg, cur.kend, smem, acc, pre);
+    else
+      mainloop<TBM, TBN, WM, WN, AK, BK_>(static_cast<const uint16_t*>(g.a), g.lda, static_cast<const uint16_t*>(g.b),
+                                          g.ldb, g.m, g.n, cur.m0, cur.n0, cur.kbeg, cur.kend, smem, acc, pre);
+    const int nu = u + gridDim.x;
+    const bool more = nu < total;
+    PUnit<TBM, TBN, WM, WN> nxt = cur;
+    if (more) nxt.decode(grp, nu);
+    bool next_pre = false;
+    if constexpr (PRE) {
+      const bool issue = more && (nxt.kend - nxt.kbeg) / BK > 0;
+      auto hook = [&]() {
+        if (issue) {
+          const K3mGemm& gn = grp.g[nxt.p];
+          Loader<AK, TBM, S::NT> la;
+          Loader<BK_, TBN, S::NT> lb;
+          la.init(static_cast<const uint16_t*>(gn.a), gn.lda, nxt.m0, nxt.kbeg, gn.m);
+          lb.init(static_cast<const uint16_t*>(gn.b), gn.ldb, nxt.n0, nxt.kbeg, gn.n);
+          la.issue(smem);
+          lb.issue(smem + TBM * BK);
+        }
+      };
+      epilogue<TBM, TBN, WM, WN, EPI, CT>(g, cur.m0, cur.n0, smem + EOFF, acc, cur.slice, hook);
+      next_pre = issue;
+    } else {
+      epilogue<TBM, TBN, WM, WN, EPI, CT>(g, cur.m0, cur.n0, smem, acc, cur.slice);
+    }
+    if (!more) break;
+    u = nu;
+    cur = nxt;
+    pre = next_pre;
   }
 }
 

@@ -471,12 +471,20 @@ int b16_cus() {
   return n;
 }
 
+// K3M_B16_PREFETCH=1: the walk issues each next tile's first k-tile inside the epilogue (A/B knob; bit-identical,
+// +0.1 % on the bf16 step, within noise: off, profiles/r3_ab_b16_persist.txt)
+const bool kB16Prefetch = k3m_env_flag("K3M_B16_PREFETCH", false);
+
 template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF>
 void persist_launch(const k3m_b16::GemmGroup& grp, hipStream_t st) {
   const int total = grp.start[grp.count];
   const int nblk = total < b16_cus() ? total : b16_cus();
-  hipLaunchKernelGGL((k3m_b16::gemm_persist_kernel<TBM, TBN, WM, WN, AK, BK_, EPI, CT, MF>), dim3(nblk),
-                     dim3(64 * WM * WN), 0, st, grp);
+  if (kB16Prefetch)
+    hipLaunchKernelGGL((k3m_b16::gemm_persist_kernel<TBM, TBN, WM, WN, AK, BK_, EPI, CT, MF, true>), dim3(nblk),
+                       dim3(64 * WM * WN), 0, st, grp);
+  else
+    hipLaunchKernelGGL((k3m_b16::gemm_persist_kernel<TBM, TBN, WM, WN, AK, BK_, EPI, CT, MF, false>), dim3(nblk),
+                       dim3(64 * WM * WN), 0, st, grp);
 }
 
 template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF>
