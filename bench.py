@@ -326,7 +326,7 @@ def main():
         dist.all_gather(gl, t)
         per_rank = [float(x) for x in gl]
         dt = max(per_rank)
-    tr.watch.flush()
+    tr.finish()
     loss = float(out["loss"])
     ms_step = 1000.0 * dt / args.steps
     value = world * B * args.steps / dt

@@ -839,7 +839,7 @@ class K3MEngine(object):
         losses = torch.zeros((4,), dtype=torch.float32, device=dev)   # mlm_t, mlm_pv, img, -
         nmax = BT + BP
         # zero-filled: rows past the device count (a hint larger than the true count) gather row 0 with
-        # row_scale 0 and add nothing to any loss or gradient; a smaller hint is caught by _check_hints
+        # row_scale 0 and add nothing to any loss or gradient; a smaller hint is caught by check_hints
         idx_m = torch.zeros((nmax,), dtype=torch.int32, device=dev)
         lab_m = torch.zeros((nmax,), dtype=torch.int64, device=dev)
         sc_m = torch.zeros((nmax,), dtype=torch.float32, device=dev)
@@ -937,10 +937,11 @@ class K3MEngine(object):
         The LayerNorm / bias-gradient slab reductions are batched (ops.deferred_reductions): flushed
         right before each grad_ready hand-off (so the all-reduce sees final gradients) and at the end."""
         with ops.deferred_reductions() as dr:
-            hook = None
-            if grad_ready is not None:
-                def hook(kind, index):
-                    dr.flush()
+            # flushed at every block boundary, with or without DDP: the slab workspaces of one block are
+            # all that is alive at a time, and they are read back soon after they were written
+            def hook(kind, index):
+                dr.flush()
+                if grad_ready is not None:
                     grad_ready(kind, index)
             self._backward(ctx, w_mlm, w_img, w_lpm, hook)
 

@@ -219,7 +219,9 @@ def linear_dgrad(dy, W, dx=None, beta=0.0, dgelu_aux=None, alpha=1.0, colsum_out
     if dx is None:
         dx = torch.empty((M, K), dtype=dy.dtype, device=dy.device)
     epi = L.EPI_DGELU if dgelu_aux is not None else L.EPI_NONE
-    s = _splitk(M, K, N, dy.dtype) if (epi == L.EPI_NONE and dx.dtype == torch.float32 and N >= 8192) else 1
+    # (no K split when the column sums of dx are wanted: the split-K path leaves no place for them)
+    s = _splitk(M, K, N, dy.dtype) if (epi == L.EPI_NONE and dx.dtype == torch.float32 and N >= 8192
+                                       and colsum_out is None) else 1
     if s > 1:
         ws = torch.empty((s * M * K,), dtype=torch.float32, device=dy.device)
         return gemm(dy, 0, W, 0, dx, M, K, N, epi, None, None, alpha, beta, s, ws)

@@ -245,6 +245,13 @@ class Trainer(object):
         fp.shadow_fresh = fresh   # frozen tensors are not updated: the shadow stays as fresh as it was
         self.global_step += 1
 
+    def finish(self):
+        """Synchronising end-of-run (or end-of-epoch) checks: every outstanding label-count hint and
+        every outstanding loss fail-fast check."""
+        self.engine.check_hints(wait=True)
+        if self.watch is not None:
+            self.watch.flush()
+
     # ---------------------------------------------------------------- checkpoints
     def save_checkpoint(self, tar_path=None, bin_path=None):
         """The reference driver's .tar / .bin files (train_concap_struc.py:691-705; k3m_amd/checkpoint.py)."""
@@ -278,6 +285,7 @@ class Trainer(object):
             self.watch.push(self.global_step, out["loss"])
         self.micro += 1
         if last:
+            eng.check_hints()   # a completed label-count check that failed raises before the update
             scale = 1.0
             if sync:
                 self.ddp.finish()

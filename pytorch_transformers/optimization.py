@@ -43,24 +43,31 @@ class AdamW(torch.optim.Optimizer):
                 npad = (n + 3) // 4 * 4
                 if not st:
                     st["step"] = 0
-                    # moments kept padded to 16 B (the kernel's vector width); the pad stays 0
-                    st["exp_avg"] = torch.zeros(npad, dtype=torch.float32, device=p.device)
-                    st["exp_avg_sq"] = torch.zeros(npad, dtype=torch.float32, device=p.device)
+                    # the reference layout: moments shaped like the parameter (state_dict interchange)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                m, v = st["exp_avg"], st["exp_avg_sq"]
+                if m.shape != p.shape or v.shape != p.shape:
+                    raise ValueError("AdamW state for a parameter of shape %s has moments of shape %s / %s"
+                                     % (tuple(p.shape), tuple(m.shape), tuple(v.shape)))
+                if not (m.is_cuda and v.is_cuda and m.dtype == torch.float32 and v.dtype == torch.float32):
+                    raise RuntimeError("AdamW moments must be HIP fp32 tensors (got %s %s)" % (m.device, m.dtype))
                 st["step"] += 1
-                direct = (npad == n and p.is_contiguous() and p.grad.is_contiguous() and p.data_ptr() % 16 == 0
-                          and p.grad.data_ptr() % 16 == 0)
+                ts = (p.data, p.grad, m, v)
+                direct = npad == n and all(t.is_contiguous() and t.data_ptr() % 16 == 0 for t in ts)
                 if direct:
-                    pp, gg = p.data, p.grad
+                    pp, gg, mm, vv = ts
                 else:
-                    pp = torch.zeros(npad, dtype=torch.float32, device=p.device)
-                    gg = torch.zeros(npad, dtype=torch.float32, device=p.device)
-                    pp[:n].copy_(p.data.reshape(-1))
-                    gg[:n].copy_(p.grad.reshape(-1))
-                L.call("k3m_adamw", pp.data_ptr(), gg.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
+                    # the kernel runs on 16-B vectors: stage padded copies (pad 0) and write the results back
+                    pp, gg, mm, vv = (torch.zeros(npad, dtype=torch.float32, device=p.device) for _ in range(4))
+                    for dst, src in zip((pp, gg, mm, vv), ts):
+                        dst[:n].copy_(src.reshape(-1))
+                L.call("k3m_adamw", pp.data_ptr(), gg.data_ptr(), mm.data_ptr(), vv.data_ptr(),
                        None, npad, float(group["lr"]), float(b1), float(b2), float(group["eps"]),
                        float(group["weight_decay"]), int(st["step"]), 1.0, L.stream())
                 if not direct:
-                    p.data.copy_(pp[:n].view_as(p.data))
+                    for dst, src in zip((p.data, m, v), (pp, mm, vv)):
+                        dst.copy_(src[:n].view_as(dst))
         return loss
 
 

@@ -163,3 +163,49 @@ def test_loader_feeds_driver_loop(dev, tmp_path):
         assert np.isfinite(float(loss))
         n += 1
     assert n == 2
+
+
+def test_standin_adamw_state_layout_roundtrip(dev):
+    """pytorch_transformers.AdamW stand-in: moments shaped like the parameter (the reference's state_dict
+    layout, train_concap_struc.py:293 resume), an odd-sized (1601-element, the image-decoder bias) tensor
+    stepped through padded staging, and a state_dict -> load_state_dict round trip that continues exactly."""
+    from pytorch_transformers.optimization import AdamW
+    from oracle.k3m_oracle import adamw_step
+    torch.manual_seed(0)
+    shapes = [(1601,), (7, 3), (64, 16)]
+    ps = [torch.nn.Parameter(torch.randn(s, device=dev)) for s in shapes]
+    grads = [[torch.randn(s, device=dev) for s in shapes] for _ in range(4)]
+    ref = [p.detach().cpu().clone() for p in ps]
+    rm = [torch.zeros_like(r) for r in ref]
+    rv = [torch.zeros_like(r) for r in ref]
+    opt = AdamW([{"params": ps, "weight_decay": 0.01}], lr=1e-3, eps=1e-8, betas=(0.9, 0.98))
+
+    def run(o, params, it):
+        for p, g in zip(params, grads[it]):
+            p.grad = g.clone()
+        o.step()
+
+    for it in range(2):
+        run(opt, ps, it)
+        for i in range(len(ps)):
+            adamw_step(ref[i], grads[it][i].cpu(), rm[i], rv[i], it + 1, 1e-3, 0.01, 0.9, 0.98, 1e-8)
+    sd = opt.state_dict()
+    for i, s in enumerate(shapes):
+        st = sd["state"][i]
+        assert tuple(st["exp_avg"].shape) == s and tuple(st["exp_avg_sq"].shape) == s and st["step"] == 2
+    ps2 = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    opt2 = AdamW([{"params": ps2, "weight_decay": 0.01}], lr=1e-3, eps=1e-8, betas=(0.9, 0.98))
+    opt2.load_state_dict(sd)
+    for it in range(2, 4):
+        run(opt2, ps2, it)
+        for i in range(len(ps)):
+            adamw_step(ref[i], grads[it][i].cpu(), rm[i], rv[i], it + 1, 1e-3, 0.01, 0.9, 0.98, 1e-8)
+    for i in range(len(ps)):
+        np.testing.assert_allclose(ps2[i].detach().cpu().numpy(), ref[i].numpy(), rtol=2e-6, atol=1e-7)
+        np.testing.assert_allclose(opt2.state[ps2[i]]["exp_avg"].cpu().numpy(), rm[i].numpy(), rtol=2e-6, atol=1e-9)
+    bad = torch.nn.Parameter(torch.zeros(1601, device=dev))
+    opt3 = AdamW([bad], lr=1e-3)
+    opt3.state[bad] = {"step": 1, "exp_avg": torch.zeros(1604, device=dev), "exp_avg_sq": torch.zeros(1604, device=dev)}
+    bad.grad = torch.ones_like(bad)
+    with pytest.raises(ValueError, match="moments"):
+        opt3.step()

@@ -158,7 +158,12 @@ def main(argv=None):
     if "roberta" in args.model_name:
         config.model = "roberta"
     if args.freeze > config.t_biattention_id[0]:
-        config.fixed_t_layer = config.t_biattention_id[0]
+        # the reference then sets config.fixed_t_layer = t_biattention_id[0] (:206-207): the text layers below the
+        # first co-attention run under no_grad, which also cuts the embeddings' gradient.  The wide engine does not
+        # implement that truncated backward; refuse instead of training a different model.
+        raise SystemExit("--freeze %d > t_biattention_id[0] = %d (fixed_t_layer) is not supported by the MI355X "
+                         "engine; use --freeze <= %d" % (args.freeze, config.t_biattention_id[0],
+                                                         config.t_biattention_id[0]))
     config.with_coattention = args.with_coattention
     config.dynamic_attention = args.dynamic_attention
     config.if_pre_sampling = args.if_pre_sampling
@@ -192,7 +197,9 @@ def main(argv=None):
     if args.freeze != -1:
         keep = [n for n in bert_weight_name if "embeddings" in n or
                 ("encoder" in n and int(n.split(".")[2]) <= args.freeze)]
-        frozen = [n for n in names if (("module." + n) if distributed else n)[12:] in set(keep)]
+        # the reference's freeze loop runs on the unwrapped model, before the DDP wrap (:254-257 vs :308):
+        # the key never carries "module." there, in any mode
+        frozen = [n for n in names if n[12:] in set(keep)]
     lr_mult = bert_lr_mult(names, bert_weight_name, ddp=distributed) if args.pretrained_model_path else None
 
     num_dataset = 0
@@ -280,6 +287,7 @@ def main(argv=None):
             steps_done += 1
             if args.k3m_max_steps and steps_done >= args.k3m_max_steps:
                 break
+        trainer.finish()   # the epoch's outstanding label-count / loss checks (synchronising)
         if args.do_eval and valid_loader is not None:
             logger.info(f"[Epoch-{epoch}] Starting evaluation ...")
             for step, (batch, _ids) in enumerate(valid_loader.batches()):
@@ -294,8 +302,7 @@ def main(argv=None):
             trainer.save_checkpoint(tar_path=base + ".tar", bin_path=base + ".bin")
         if args.k3m_max_steps and steps_done >= args.k3m_max_steps:
             break
-    if trainer.watch is not None:
-        trainer.watch.flush()
+    trainer.finish()
     if loss_log:
         loss_log.close()
     if distributed:
