@@ -84,6 +84,8 @@ def parse():
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL) for real runs; gloo only to rehearse the "
                     "multi-rank path with several ranks sharing one GPU")
     ap.add_argument("--master-port", type=int, default=0)
+    ap.add_argument("--ddp", action="store_true", help="run the data-parallel path (process group, bucketed "
+                    "all-reduce on the comm stream) even at one rank: exercises RCCL at world size 1")
     return ap.parse_args()
 
 
@@ -274,8 +276,12 @@ def main():
     dtype = args.dtype or shape["dtype"]
     B = args.batch or shape["B"]
     dist = None
-    if world > 1:
+    use_dist = world > 1 or args.ddp
+    if use_dist:
         import torch.distributed as dist
+        if "WORLD_SIZE" not in os.environ:   # --ddp at one rank without a launcher
+            os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                              MASTER_PORT=str(args.master_port or free_port()))
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -288,7 +294,7 @@ def main():
     cfg = pretrain_config(os.path.join(HERE, "configs", "bert_base_6layer_6conect.json"))
     tr = Trainer(cfg, dev, lr=1e-4, warmup_steps=max(1, (args.steps + args.warmup) // 10),
                  total_steps=10 * (args.steps + args.warmup), seed=1234, init=True, dtype=dtype)
-    if world > 1:
+    if use_dist:
         ddp = GradAllReducer(tr.engine.fp, comm_dtype=torch.bfloat16 if dtype == "bf16" else None)
         ddp.broadcast_params(tr.engine.fp)
         tr.ddp = ddp
@@ -302,7 +308,7 @@ def main():
     cprobe.install()
 
     def barrier():
-        if world > 1:
+        if use_dist:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -320,7 +326,7 @@ def main():
     dt = time.perf_counter() - t0
     probe.active = cprobe.active = False
     per_rank = [dt]
-    if world > 1:
+    if use_dist:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         gl = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(gl, t)
@@ -377,7 +383,7 @@ def main():
                    "frac": round(co_flops / (co_ms * 1e-3) / peak, 4) if co_ms else None,
                    "scope": "18 co-attention layers fwd+bwd (lock-step blocks incl. attention and LayerNorm)"},
     }
-    if world > 1:
+    if use_dist:
         res["per_rank_s"] = [round(x, 4) for x in per_rank]
         res["backend"] = args.backend
         res["world_size_seen"] = dist.get_world_size()
@@ -402,7 +408,7 @@ def main():
         print("rank %d/%d: %.3f samples/s/GPU (%.1f ms/step)" % (rank, world, B * args.steps / per_rank[rank],
                                                                 1000.0 * per_rank[rank] / args.steps),
               file=sys.stderr, flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

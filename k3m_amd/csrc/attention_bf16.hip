@@ -20,6 +20,8 @@
 // (seed, off + ((s nh + h) lq + i) lk + j), so a mask drawn by one kernel is the other's mask.
 #include "common.h"
 
+#include <algorithm>
+
 namespace {
 
 constexpr int NW = 4, NT = NW * 64;
@@ -378,6 +380,241 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kernel(const uint16_t* __rest
     }
 }
 
+// ------------------------------------------------------------------ backward, keys on the lanes
+// The default backward (flash_bwd_kernel above holds P and dS as two [LQ][LK] LDS images: 132 KB at
+// L = 128, one 4-wave workgroup per CU).  Here the probabilities never leave the registers:
+//   key phase   wave w owns keys j0 = 32 w .. +31 on the MFMA lanes (its K and V rows are B-operand
+//               fragments in registers, loaded straight from global); per 32-query tile
+//                 S = Q K^T, dP = dO V^T            (A = Q / dO rows from LDS, 16-B reads)
+//                 P = exp(scale S + mask - LSE), Pd = P m, dS = P (dP m - D)     (in accumulators)
+//                 dV^T += dO^T Pd, dK^T += Q^T dS   (A = transposed LDS reads in the accumulator k
+//                                                    order, B = the accumulators themselves)
+//               and dS stays packed (bf16) in registers;
+//   dS^T image  written once to LDS over the Q / dO images (every wave is past its last read);
+//   query phase dQ = scale dS K per 32-query tile (A = dS from the transposed image, B = K from LDS).
+// LDS at L = 128, d = 64: Q + dO + K = 48 KB (+ 1.5 KB vectors): two or three workgroups per CU instead
+// of one.  Same semantics and dropout counters as flash_bwd_kernel / the forward.
+template <int NC>
+__device__ __forceinline__ bf16x8 trfrag_n(const uint16_t* img, int nc, int rbase, int cbase, int lane) {
+  if (nc == 4) return trfrag<4, false>(img, rbase, cbase, lane);
+  if (nc == 8) return trfrag<8, false>(img, rbase, cbase, lane);
+  return trfrag<16, false>(img, rbase, cbase, lane);
+}
+__device__ __forceinline__ int ioff_n(int nc, int r, int c) {
+  return nc == 4 ? ioff<4>(r, c) : nc == 8 ? ioff<8>(r, c) : ioff<16>(r, c);
+}
+
+// rows [row0, row0 + nrows) x [coff, coff + 8 NCS) of a bf16 matrix -> image with NCI chunks per row
+// (rows >= nvalid zero), NTH threads, every load issued before the LDS writes
+template <int NCS, int NCI, int NTH>
+__device__ __forceinline__ void stage_n(uint16_t* img, const uint16_t* __restrict__ src, long long row0, long long ld,
+                                        int coff, int nrows, int nvalid) {
+  constexpr int U = (MAXL * NCS + NTH - 1) / NTH;
+  uint4 r[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = threadIdx.x + u * NTH;
+    const int i = e / NCS, c = e % NCS;
+    r[u] = make_uint4(0u, 0u, 0u, 0u);
+    if (i < nvalid) r[u] = *reinterpret_cast<const uint4*>(src + (row0 + i) * ld + coff + 8 * c);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = threadIdx.x + u * NTH;
+    const int i = e / NCS, c = e % NCS;
+    if (i < nrows) *reinterpret_cast<uint4*>(img + ioff<NCI>(i, c)) = r[u];
+  }
+}
+
+template <int HD>
+constexpr int km_occupancy() { return HD == 64 ? 2 : 1; }
+
+template <int HD, int NW>
+__global__ __launch_bounds__(NW * 64, km_occupancy<HD>()) void flash_bwd_km_kernel(
+    const uint16_t* __restrict__ dctx, long long ldc, const uint16_t* __restrict__ o, long long ldo,
+    const uint16_t* __restrict__ q, long long ldq, const uint16_t* __restrict__ k, long long ldk,
+    const uint16_t* __restrict__ v, long long ldv, const float* __restrict__ kmask, const float* __restrict__ lse,
+    uint16_t* __restrict__ dq, uint16_t* __restrict__ dk, uint16_t* __restrict__ dv, long long lddq, long long lddk,
+    long long lddv, int lq, int lk, int nh, float scale, float p_drop, uint64_t seed, uint64_t off) {
+  constexpr int NTH = NW * 64;
+  constexpr int NCL = HD / 8, NC = HD == 96 ? 16 : HD / 8, DT = HD / 32, KS = HD / 16;
+  constexpr int HW = NC * 8;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int s = blockIdx.x / nh, h = blockIdx.x % nh;
+  const int LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
+  const int QW = LQ == 96 ? 128 : LQ, QNC = QW / 8;      // dS^T image [LK][QW]
+  const int RQ = max(2 * LQ * HW, LK * QW);               // the region shared by Q | dO and dS^T
+  uint16_t* Qs = smem;
+  uint16_t* dOs = Qs + LQ * HW;
+  uint16_t* dSt = smem;
+  uint16_t* Ks = smem + RQ;
+  float* msk = reinterpret_cast<float*>(Ks + LK * HW);
+  float* Ls = msk + LK;
+  float* Ds = Ls + LQ;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
+  const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
+  const int hoff = h * HD;
+  const long long lrow0 = ((long long)s * nh + h) * lq;
+  const K3mDrop dr = k3m_drop_init(seed, p_drop);
+  const int NQT = LQ >> 5;
+
+  // this wave's key tile: K and V rows as B-operand fragments (lane -> key j, 8 consecutive d)
+  const int j = 32 * w + cl;
+  const bool kw = 32 * w < LK;   // wave-uniform
+  bf16x8 kf[KS], vf[KS];
+  {
+    const bool ok = kw && j < lk;
+    const uint16_t* kp = k + (krow0 + (ok ? j : 0)) * ldk + hoff + 8 * kl;
+    const uint16_t* vp = v + (krow0 + (ok ? j : 0)) * ldv + hoff + 8 * kl;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const uint4 a = ok ? *reinterpret_cast<const uint4*>(kp + 16 * ks) : make_uint4(0u, 0u, 0u, 0u);
+      const uint4 b = ok ? *reinterpret_cast<const uint4*>(vp + 16 * ks) : make_uint4(0u, 0u, 0u, 0u);
+      kf[ks] = __builtin_bit_cast(bf16x8, a);
+      vf[ks] = __builtin_bit_cast(bf16x8, b);
+    }
+  }
+  stage_n<NCL, NC, NTH>(Qs, q, qrow0, ldq, hoff, LQ, lq);
+  stage_n<NCL, NC, NTH>(dOs, dctx, qrow0, ldc, hoff, LQ, lq);
+  stage_n<NCL, NC, NTH>(Ks, k, krow0, ldk, hoff, LK, lk);
+  for (int jj = threadIdx.x; jj < LK; jj += NTH) msk[jj] = jj < lk ? (kmask ? kmask[krow0 + jj] : 0.f) : -INFINITY;
+  for (int ii = threadIdx.x >> 1; ii < LQ; ii += NTH / 2) {
+    // D_i = dO_i . O_i: two threads per row, each over half of the head dimension (16-B loads)
+    const int half = threadIdx.x & 1;
+    float acc = 0.f;
+    if (ii < lq) {
+      const uint16_t* pd = dctx + (qrow0 + ii) * ldc + hoff + half * (HD / 2);
+      const uint16_t* po = o + (qrow0 + ii) * ldo + hoff + half * (HD / 2);
+      uint4 a[HD / 16], b[HD / 16];
+#pragma unroll
+      for (int c = 0; c < HD / 16; ++c) {
+        a[c] = *reinterpret_cast<const uint4*>(pd + 8 * c);
+        b[c] = *reinterpret_cast<const uint4*>(po + 8 * c);
+      }
+#pragma unroll
+      for (int c = 0; c < HD / 16; ++c) {
+        const uint32_t wa[4] = {a[c].x, a[c].y, a[c].z, a[c].w}, wb[4] = {b[c].x, b[c].y, b[c].z, b[c].w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          acc += __uint_as_float(wa[t] << 16) * __uint_as_float(wb[t] << 16) +
+                 __uint_as_float(wa[t] & 0xffff0000u) * __uint_as_float(wb[t] & 0xffff0000u);
+      }
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    if (half == 0) {
+      Ds[ii] = acc;
+      Ls[ii] = ii < lq ? lse[lrow0 + ii] : INFINITY;   // padding query rows: P = exp(-inf) = 0
+    }
+  }
+  __syncthreads();
+
+  uint32_t dsp[MAXL / 32][8];   // dS of each query tile, bf16 pairs (registers 2t, 2t + 1)
+  if (kw) {
+    const float mj = msk[j];
+    floatx16 dV[DT], dK[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      dV[dt] = zero16();
+      dK[dt] = zero16();
+    }
+#pragma unroll
+    for (int it = 0; it < MAXL / 32; ++it) {
+      if (it >= NQT) break;
+      floatx16 S = zero16(), dP = zero16();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        S = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag<NC>(Qs, 32 * it, ks, lane), kf[ks], S, 0, 0, 0);
+        dP = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag<NC>(dOs, 32 * it, ks, lane), vf[ks], dP, 0, 0, 0);
+      }
+      // accumulator r holds query i = 32 it + 8 (r >> 2) + 4 kl + (r & 3), key j
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int i0 = 32 * it + 8 * a + 4 * kl;
+        const float4 l4 = *reinterpret_cast<const float4*>(Ls + i0);
+        const float4 d4 = *reinterpret_cast<const float4*>(Ds + i0);
+        const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int r = 4 * a + b, i = i0 + b;
+          const float p = __expf(S[r] * scale + mj - lv[b]);
+          const float dm = k3m_drop(dr, off + (lrow0 + min(i, lq - 1)) * lk + min(j, lk - 1));
+          S[r] = p * dm;                          // P_drop
+          dP[r] = p * (dP[r] * dm - dv4[b]);      // dS
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t) dsp[it][t] = (uint32_t)bf_bits(dP[2 * t]) | ((uint32_t)bf_bits(dP[2 * t + 1]) << 16);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 bp = accfrag(S, s2), bs = accfrag(dP, s2);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          dV[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag<NC, true>(dOs, 32 * it + 16 * s2, 32 * dt, lane), bp,
+                                                            dV[dt], 0, 0, 0);
+          dK[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag<NC, true>(Qs, 32 * it + 16 * s2, 32 * dt, lane), bs,
+                                                            dK[dt], 0, 0, 0);
+        }
+      }
+    }
+    // dV^T / dK^T: lane -> key j, register r -> d = 32 dt + 8 (r >> 2) + 4 kl + (r & 3): 8-B stores
+    if (j < lk) {
+      uint16_t* pv = dv + (krow0 + j) * lddv + hoff + 4 * kl;
+      uint16_t* pk = dk + (krow0 + j) * lddk + hoff + 4 * kl;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          uint2 wv, wk;
+          wv.x = bf_bits(dV[dt][4 * a]) | ((uint32_t)bf_bits(dV[dt][4 * a + 1]) << 16);
+          wv.y = bf_bits(dV[dt][4 * a + 2]) | ((uint32_t)bf_bits(dV[dt][4 * a + 3]) << 16);
+          wk.x = bf_bits(dK[dt][4 * a] * scale) | ((uint32_t)bf_bits(dK[dt][4 * a + 1] * scale) << 16);
+          wk.y = bf_bits(dK[dt][4 * a + 2] * scale) | ((uint32_t)bf_bits(dK[dt][4 * a + 3] * scale) << 16);
+          *reinterpret_cast<uint2*>(pv + 32 * dt + 8 * a) = wv;
+          *reinterpret_cast<uint2*>(pk + 32 * dt + 8 * a) = wk;
+        }
+    }
+  }
+  __syncthreads();   // every wave is past its last read of Q / dO
+  if (kw) {
+    // dS^T[j][i]: registers 4a..4a+3 of query tile it are queries 32 it + 8 a + 4 kl .. +3 (8 bytes)
+#pragma unroll
+    for (int it = 0; it < MAXL / 32; ++it) {
+      if (it >= NQT) break;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        *reinterpret_cast<uint2*>(dSt + ioff_n(QNC, j, 4 * it + a) + 4 * kl) = make_uint2(dsp[it][2 * a], dsp[it][2 * a + 1]);
+    }
+  }
+  __syncthreads();
+  // query phase: dQ = scale dS K, tile it of 32 queries per wave (lane -> d, registers -> queries)
+  for (int it = w; it < NQT; it += NW) {
+    floatx16 dQ[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) dQ[dt] = zero16();
+    for (int kk = 0; kk < LK / 16; ++kk) {
+      const bf16x8 a = trfrag_n<NC>(dSt, QNC, 16 * kk, 32 * it, lane);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+        dQ[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, trfrag<NC, false>(Ks, 16 * kk, 32 * dt, lane), dQ[dt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ii = 32 * it + (r & 3) + 8 * (r >> 2) + 4 * kl;
+        if (ii < lq) dq[(qrow0 + ii) * lddq + hoff + 32 * dt + cl] = bf_bits(dQ[dt][r] * scale);
+      }
+  }
+}
+
+size_t bwd_km_lds(int lq, int lk, int hd) {
+  const size_t LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
+  if (hd == 96) hd = 128;
+  const size_t QW = LQ == 96 ? 128 : LQ;
+  return 2 * (std::max(2 * LQ * hd, LK * QW) + LK * hd) + 4 * (LK + 2 * LQ);
+}
+
 size_t fwd_lds(int lq, int lk, int hd) {
   const size_t LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
   if (hd == 96) hd = 128;
@@ -401,6 +638,12 @@ void set_attrs() {
     (void)hipFuncSetAttribute((const void*)flash_bwd_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_bwd_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_bwd_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_bwd_km_kernel<64, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_bwd_km_kernel<64, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_bwd_km_kernel<96, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_bwd_km_kernel<96, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_bwd_km_kernel<128, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_bwd_km_kernel<128, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     done = true;
   }
 }
@@ -408,6 +651,9 @@ void set_attrs() {
 bool vec_ok(const void* p, long long ld) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 8 == 0; }
 
 }  // namespace
+
+// the key-major backward (flash_bwd_km_kernel); K3M_FLASH_BWD_KM=0 keeps the P / dS image kernel
+static const bool kFlashBwdKM = k3m_env_flag("K3M_FLASH_BWD_KM", true);
 
 extern "C" int k3m_flash_attn_fwd(const void* q, long long ldq, const void* k, long long ldk, const void* v,
                                   long long ldv, const float* kmask, void* ctx, long long ldc, float* lse, int nseq,
@@ -446,9 +692,29 @@ extern "C" int k3m_flash_attn_bwd(const void* dctx, long long ldc, const void* o
   K3M_ARG(lq > 0 && lq <= MAXL && lk > 0 && lk <= MAXL && (hd == 64 || hd == 96 || hd == 128) && nh > 0 && nseq >= 0);
   K3M_ARG(vec_ok(q, ldq) && vec_ok(k, ldk) && vec_ok(v, ldv) && vec_ok(dctx, ldc) && vec_ok(o, ldo));
   if (nseq == 0) return 0;
+  set_attrs();
+  if (kFlashBwdKM && vec_ok(dk, lddk) && vec_ok(dv, lddv)) {
+    const size_t lk_lds = bwd_km_lds(lq, lk, hd);
+    K3M_ARG(lk_lds <= (size_t)LDS_MAX);
+#define K3M_FLASH_BWD_KM(HD_, NW_)                                                                                     \
+  hipLaunchKernelGGL((flash_bwd_km_kernel<HD_, NW_>), dim3(nseq * nh), dim3(NW_ * 64), lk_lds, st, (const uint16_t*)dctx, \
+                     ldc, (const uint16_t*)o, ldo, (const uint16_t*)q, ldq, (const uint16_t*)k, ldk, (const uint16_t*)v, \
+                     ldv, kmask, lse, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, lddq, lddk, lddv, lq, lk, nh, scale,   \
+                     p_drop, seed, off)
+    const bool two = lk <= 64;   // two waves own the key tiles of a short head: smaller workgroups, more per CU
+    if (hd == 64) {
+      if (two) K3M_FLASH_BWD_KM(64, 2); else K3M_FLASH_BWD_KM(64, 4);
+    } else if (hd == 96) {
+      if (two) K3M_FLASH_BWD_KM(96, 2); else K3M_FLASH_BWD_KM(96, 4);
+    } else {
+      if (two) K3M_FLASH_BWD_KM(128, 2); else K3M_FLASH_BWD_KM(128, 4);
+    }
+#undef K3M_FLASH_BWD_KM
+    K3M_CHECK_LAUNCH();
+    return 0;
+  }
   const size_t lds = bwd_lds(lq, lk, hd);
   K3M_ARG(lds <= (size_t)LDS_MAX);
-  set_attrs();
   if (hd == 96)
     hipLaunchKernelGGL(flash_bwd_kernel<96>, dim3(nseq * nh), dim3(NT), lds, st, (const uint16_t*)dctx, ldc,
                        (const uint16_t*)o, ldo, (const uint16_t*)q, ldq, (const uint16_t*)k, ldk, (const uint16_t*)v,

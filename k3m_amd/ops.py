@@ -458,13 +458,23 @@ def _short_fits(lq, lk, hd, bwd):
     return 4 * (LQ * hd + r2n + LQ * LK + (0 if LK * hd + LQ <= r2n else LQ)) <= LDS_MAX
 
 
+# attention_bf16.hip: the key-major backward (flash_bwd_km_kernel, default) or the P / dS image kernel
+FLASH_BWD_KM = os.environ.get("K3M_FLASH_BWD_KM", "1") != "0"
+
+
 def flash_fits(lq, lk, hd):
-    """attention_bf16.hip's LDS images (its fwd_lds / bwd_lds; the backward is the larger) fit 160 KB."""
+    """attention_bf16.hip's LDS images (fwd_lds and bwd_km_lds / bwd_lds there) fit 160 KB."""
     if max(lq, lk) > SHORT_MAXL or hd not in (64, 96, 128):
         return False
     LQ, LK, h = _r32(lq), _r32(lk), 128 if hd == 96 else hd
-    PW = 128 if LK == 96 else LK
-    return 2 * (2 * LQ * h + 2 * LK * h + 2 * LQ * PW) + 4 * (LK + 2 * LQ) <= LDS_MAX
+    fwd = 2 * (LQ * h + 2 * LK * h) + 4 * LK
+    if FLASH_BWD_KM:
+        QW = 128 if LQ == 96 else LQ
+        bwd = 2 * (max(2 * LQ * h, LK * QW) + LK * h) + 4 * (LK + 2 * LQ)
+    else:
+        PW = 128 if LK == 96 else LK
+        bwd = 2 * (2 * LQ * h + 2 * LK * h + 2 * LQ * PW) + 4 * (LK + 2 * LQ)
+    return max(fwd, bwd) <= LDS_MAX
 
 
 def attn_fwd(q, k, v, kmask, ctx, probs, nseq, lq, lk, nh, hd, scale, p_drop, seed, off):

@@ -61,6 +61,10 @@ for s in "$@"; do
     pmcdata) export TMPDIR=/tmp
          step pmcd_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcd_fetch -o run -- python scripts/bench_data.py --reps 20
          step pmcd_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcd_write -o run -- python scripts/bench_data.py --reps 20 ;;
+    flash) step flash 400 python -u -m pytest tests/test_gpu_gemm_bf16.py -k flash -q --timeout 120 --timeout-method thread ;;
+    rccl) step rccl 900 python -u -m pytest tests/test_gpu_rccl.py -v -s --timeout 300 --timeout-method thread ;;
+    standin) step standin 300 python -u -m pytest tests/test_gpu_dropin.py -q --timeout 200 --timeout-method thread ;;
+    abkm) step abkm 900 scripts/ab_env.sh K3M_FLASH_BWD_KM "0 1" 3 --config 3 --steps 10 --warmup 4 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -205,7 +205,8 @@ def test_attention_bf16(dev, lq, lk, nh, hd):
 @pytest.mark.parametrize("lq,lk,nh,hd", [(36, 36, 12, 64), (128, 128, 12, 64), (37, 37, 8, 128), (36, 37, 8, 128),
                                          (128, 37, 8, 128), (37, 128, 8, 128), (128, 36, 8, 128), (20, 90, 4, 64),
                                          (128, 36, 8, 96), (36, 128, 8, 96),
-                                         (1, 5, 2, 64)])
+                                         (1, 5, 2, 64), (128, 101, 8, 128), (128, 128, 8, 128), (96, 128, 12, 64),
+                                         (65, 128, 4, 64), (128, 128, 8, 96), (33, 64, 3, 64)])
 def test_flash_attention_bf16(dev, lq, lk, nh, hd):
     """LSE-saving bf16 attention (attention_bf16.hip) against fp32 math on the same bf16 inputs,
     and, with dropout on, against the probability-saving kernel drawing the same mask."""
