@@ -169,17 +169,29 @@ class CoattnProbe(object):
         return sum(s.elapsed_time(e) for s, e in self.events)
 
 
-def pmc_traffic(key, kernel_prefix):
-    """HBM-side bytes per launch of the probed GEMM from a committed rocprofv3 PMC record
-    (profiles/*_gemm_ffn1_pmc.json: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), or None."""
+def head_kernel(bf):
+    """Full-name fragment of the kernel the probed GEMM runs at HEAD with the default knobs (gemm.hip /
+    gemm_bf16.hip dispatch of a 256x256-tile problem of >= K3M_*_PERSIST_MIN blocks)."""
+    if bf:
+        return "k3m_b16::gemm_persist_kernel<256, 256" if os.environ.get("K3M_B16_PERSIST", "1") != "0" \
+            else "k3m_b16::gemm_kernel<256, 256"
+    return "k3m_x6::gemm_x6_persist_kernel<256, 256" if os.environ.get("K3M_X6_PERSIST", "1") != "0" \
+        else "k3m_x6::gemm_x6_kernel<256, 256"
+
+
+def pmc_traffic(key, kernel):
+    """HBM-side bytes per launch of the probed GEMM from the newest committed rocprofv3 PMC record of THIS
+    kernel and shape (profiles/r*_pmc_*.json from scripts/pmc_gemm.sh + scripts/pmc_table.py: FETCH_SIZE x2
+    gfx950 correction + WRITE_SIZE), or None."""
     import glob
-    for path in sorted(glob.glob(os.path.join(HERE, "profiles", "*_gemm_ffn1_pmc.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(HERE, "profiles", "r*pmc*.json")), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        if tuple(d.get("shape", ())) == tuple(key) and kernel_prefix in d.get("kernel", ""):
+        names = d.get("kernel_names") or [d.get("kernel", "")]
+        if tuple(d.get("shape") or ()) == tuple(key) and d.get("traffic_bytes") and any(kernel in n for n in names):
             return int(d["traffic_bytes"]), os.path.relpath(path, HERE)
     return None, None
 
@@ -195,16 +207,34 @@ def cpu_model():
     return "unknown"
 
 
+def cpu_share():
+    """Threads for the CPU baseline = this process's CPU share: the affinity mask (os.sched_getaffinity),
+    capped by the cgroup's CPU quota (cpu.max) when one is set — on the GPU box nproc / os.cpu_count()
+    report the whole machine.  Returns (threads, how it was determined)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    n = min(aff, quota) if quota else aff
+    return n, "sched_getaffinity=%d, cgroup cpu.max=%s, nproc=%d" % (aff, quota if quota else "max",
+                                                                      os.cpu_count() or 0)
+
+
 def cpu_baseline(cfg, shape, bsz, steps):
     """Oracle (torch CPU fp32) fwd+bwd+AdamW on a bounded sample of the same workload; baseline only.
-    Threads: this process's CPU share on the GPU box (OMP_NUM_THREADS, 16 per GPU there), not the
-    machine's nproc (reported beside it).  One bs=8 warm-up step, a bs=8 sample (2 timed steps), then
+    Threads: this process's CPU share on the GPU box (os.sched_getaffinity), not the machine's nproc
+    (reported beside it).  One bs=8 warm-up step, a bs=8 sample (2 timed steps), then
     ``steps`` timed steps at ``bsz`` (the GPU workload's batch)."""
     import torch
     from oracle import k3m_oracle as O
     from k3m_amd.weights import init_values
     from k3m_amd.synthetic import synthetic_batch, synthetic_noise
-    ncores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    ncores, share = cpu_share()
     torch.set_num_threads(ncores)
     P = {k: torch.from_numpy(v).requires_grad_(True) for k, v in init_values(cfg, 0).items()}
     T, Pl, nbox = shape["T"], shape["P"], shape["nbox"]
@@ -252,7 +282,7 @@ def cpu_baseline(cfg, shape, bsz, steps):
         step(big)
     dt = time.perf_counter() - t0
     return {"value": round(bsz * steps / dt, 4), "unit": "samples/s", "cores": ncores, "kind": "port",
-            "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+            "nproc": os.cpu_count(), "cpu_share": share, "cpu_model": cpu_model(),
             "bs8_samples_s": round(8 * 2 / dt8, 4),
             "sample": "oracle/k3m_oracle.py fwd+bwd+AdamW, fp32, bs=%d, %d timed step(s) (%.1f s) after a bs=8 warm-up; "
                       "bs=8: 2 timed steps %.1f s (same shapes as the GPU workload; torch CPU, %d threads = this "
@@ -344,7 +374,7 @@ def main():
     from k3m_amd import ops as _ops, _lib as _L
     x6 = not bf and _ops.F32_ALGO == _L.F32_SPLIT_BF16X6
     peak = PEAK_BF16_MFMA if bf else (PEAK_F32_X6 if x6 else PEAK_F32_MFMA)
-    kname = "gemm_bf16_kernel" if bf else ("gemm_x6_kernel" if x6 else "gemm_f32_kernel")
+    kname = head_kernel(bf) if (bf or x6) else "gemm_f32_kernel"
     traffic, traffic_src = pmc_traffic(probe.key, kname)
     ref_sample = 3.0 * ref_fwd_flops(T, P, R, shape["n_triples"])
     co_flops = 3.0 * coattn_fwd_flops(T, P, R) * B

@@ -65,19 +65,10 @@ typedef struct K3mGemm {
   float* ws;             /* splitk > 1: fp32 workspace of splitk*m*n floats (deterministic    */
   float alpha, beta;     /* slab reduction, no atomics)                                        */
   int f32_algo;          /* fp32 operands: K3M_F32_SPLIT_BF16X6 (0, default) or K3M_F32_MFMA_F32 */
-  long long a_planes;    /* 0: A holds fp32 values.  > 0 (with b_planes > 0, dtype K3M_F32): A is given    */
-  long long b_planes;    /* PRE-SPLIT, as the three exact bf16 planes of k3m_split3 — a points at the h   */
-                         /* plane (leading dimension lda, in elements), m and l follow at +a_planes and  */
-                         /* +2*a_planes elements; likewise B.  The bf16x6 products are then staged by    */
-                         /* LDS-DMA with no split in the kernel; bit-identical to splitting in-kernel.   */
+  long long a_planes;    /* reserved, must be 0 */
+  long long b_planes;    /* reserved, must be 0 */
 } K3mGemm;
 int k3m_gemm(const K3mGemm* g, hipStream_t stream);
-/* The exact three-way split of an fp32 matrix for K3mGemm.a_planes / b_planes: x = h + m + l with
- * h = rne_bf16(x), m = rne_bf16(x - h), l = x - h - m (exact), written as bf16 planes h at planes,
- * m at planes + pstride, l at planes + 2*pstride elements, each [rows][ldp].  cols % 8 == 0,
- * 16-B aligned rows. */
-int k3m_split3(const float* x, long long ldx, int rows, int cols, void* planes, long long ldp, long long pstride,
-               hipStream_t stream);
 /* OR-ed into K3mGemm.epilogue of a split-K GEMM (splitk > 1, epilogue NONE): the kernel writes its fp32
  * slabs (ws[slice][m][n], raw sums) and returns without reducing them — C is untouched.  The caller
  * reduces them later with k3m_slab_reduce_batch (nslab = splitk, cols = m*n, requires ldc == n,

@@ -34,7 +34,6 @@ class K3mGemm(C.Structure):
 # name -> argtypes (restype is always int status)
 SIGNATURES = {
     "k3m_gemm": [C.POINTER(K3mGemm), vp],
-    "k3m_split3": [vp, i64, i32, i32, vp, i64, i64, vp],
     "k3m_colsum": [vp, i64, i32, i32, vp, i32, vp, i32, vp],
     "k3m_ln_fwd": [vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, f32, u64, u64, u64, i32, vp],
     "k3m_ln_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, u64, u64, u64, i32, vp, i32, vp],

@@ -124,10 +124,34 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __rest
   const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
   const int hoff = h * HD;
 
-  stage<NCL, NC>(Qs, q, qrow0, ldq, hoff, LQ, lq);
-  stage<NCL, NC>(Ks, k, krow0, ldk, hoff, LK, lk);
-  stage<NCL, NC>(Vs, v, krow0, ldv, hoff, LK, lk);
-  for (int j = threadIdx.x; j < LK; j += NT) msk[j] = j < lk ? (kmask ? kmask[krow0 + j] : 0.f) : -INFINITY;
+  {
+    // every global load (Q, K, V chunks, mask) issued before the first LDS write: one memory round trip
+    constexpr int U = MAXL * NCL / NT;
+    uint4 rq[U], rk[U], rv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = threadIdx.x + u * NT, i = e / NCL, c = e % NCL;
+      const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+      const bool qv = i < lq, kv = i < lk;
+      const long long qo = qrow0 + (qv ? i : 0), ko = krow0 + (kv ? i : 0);
+      rq[u] = qv ? *reinterpret_cast<const uint4*>(q + qo * ldq + hoff + 8 * c) : z;
+      rk[u] = kv ? *reinterpret_cast<const uint4*>(k + ko * ldk + hoff + 8 * c) : z;
+      rv[u] = kv ? *reinterpret_cast<const uint4*>(v + ko * ldv + hoff + 8 * c) : z;
+    }
+    const int t = threadIdx.x;
+    float mv = 0.f;
+    if (t < LK) mv = t < lk ? (kmask ? kmask[krow0 + t] : 0.f) : -INFINITY;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = threadIdx.x + u * NT, i = e / NCL, c = e % NCL;
+      if (i < LQ) *reinterpret_cast<uint4*>(Qs + ioff<NC>(i, c)) = rq[u];
+      if (i < LK) {
+        *reinterpret_cast<uint4*>(Ks + ioff<NC>(i, c)) = rk[u];
+        *reinterpret_cast<uint4*>(Vs + ioff<NC>(i, c)) = rv[u];
+      }
+    }
+    if (t < LK) msk[t] = mv;
+  }
   __syncthreads();
   const int i0 = 32 * w;
   if (i0 >= LQ) return;
@@ -451,6 +475,7 @@ __global__ __launch_bounds__(NW * 64, km_occupancy<HD>()) void flash_bwd_km_kern
   float* msk = reinterpret_cast<float*>(Ks + LK * HW);
   float* Ls = msk + LK;
   float* Ds = Ls + LQ;
+  float* scr = Ds + LQ;   // [LQ][NCL] chunk dot products of dO and O
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
   const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
@@ -475,36 +500,51 @@ __global__ __launch_bounds__(NW * 64, km_occupancy<HD>()) void flash_bwd_km_kern
       vf[ks] = __builtin_bit_cast(bf16x8, b);
     }
   }
-  stage_n<NCL, NC, NTH>(Qs, q, qrow0, ldq, hoff, LQ, lq);
-  stage_n<NCL, NC, NTH>(dOs, dctx, qrow0, ldc, hoff, LQ, lq);
-  stage_n<NCL, NC, NTH>(Ks, k, krow0, ldk, hoff, LK, lk);
-  for (int jj = threadIdx.x; jj < LK; jj += NTH) msk[jj] = jj < lk ? (kmask ? kmask[krow0 + jj] : 0.f) : -INFINITY;
-  for (int ii = threadIdx.x >> 1; ii < LQ; ii += NTH / 2) {
-    // D_i = dO_i . O_i: two threads per row, each over half of the head dimension (16-B loads)
-    const int half = threadIdx.x & 1;
-    float acc = 0.f;
-    if (ii < lq) {
-      const uint16_t* pd = dctx + (qrow0 + ii) * ldc + hoff + half * (HD / 2);
-      const uint16_t* po = o + (qrow0 + ii) * ldo + hoff + half * (HD / 2);
-      uint4 a[HD / 16], b[HD / 16];
+  {
+    // prologue: every global load (Q, dO, O, K chunks; mask; LSE) issued before the first LDS write, so
+    // the workgroup waits for one memory round trip, not four.  Thread t takes chunks e = t + u NTH
+    // (row e / NCL, chunk e % NCL); D_i = dO_i . O_i from per-chunk dot products summed over the row.
+    constexpr int U = (MAXL * NCL + NTH - 1) / NTH;
+    uint4 rq[U], rdo[U], ro[U], rk[U];
 #pragma unroll
-      for (int c = 0; c < HD / 16; ++c) {
-        a[c] = *reinterpret_cast<const uint4*>(pd + 8 * c);
-        b[c] = *reinterpret_cast<const uint4*>(po + 8 * c);
-      }
-#pragma unroll
-      for (int c = 0; c < HD / 16; ++c) {
-        const uint32_t wa[4] = {a[c].x, a[c].y, a[c].z, a[c].w}, wb[4] = {b[c].x, b[c].y, b[c].z, b[c].w};
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-          acc += __uint_as_float(wa[t] << 16) * __uint_as_float(wb[t] << 16) +
-                 __uint_as_float(wa[t] & 0xffff0000u) * __uint_as_float(wb[t] & 0xffff0000u);
-      }
+    for (int u = 0; u < U; ++u) {
+      const int e = threadIdx.x + u * NTH, i = e / NCL, c = e % NCL;
+      const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+      const bool qv = i < lq, kv = i < lk;
+      const long long qo = (qrow0 + (qv ? i : 0)), ko = (krow0 + (kv ? i : 0));
+      rq[u] = qv ? *reinterpret_cast<const uint4*>(q + qo * ldq + hoff + 8 * c) : z;
+      rdo[u] = qv ? *reinterpret_cast<const uint4*>(dctx + qo * ldc + hoff + 8 * c) : z;
+      ro[u] = qv ? *reinterpret_cast<const uint4*>(o + qo * ldo + hoff + 8 * c) : z;
+      rk[u] = kv ? *reinterpret_cast<const uint4*>(k + ko * ldk + hoff + 8 * c) : z;
     }
-    acc += __shfl_xor(acc, 1, 64);
-    if (half == 0) {
-      Ds[ii] = acc;
-      Ls[ii] = ii < lq ? lse[lrow0 + ii] : INFINITY;   // padding query rows: P = exp(-inf) = 0
+    float mv = 0.f, lv = 0.f;
+    const int t = threadIdx.x;
+    if (t < LK) mv = t < lk ? (kmask ? kmask[krow0 + t] : 0.f) : -INFINITY;
+    if (t < LQ) lv = t < lq ? lse[lrow0 + t] : INFINITY;   // padding query rows: P = exp(-inf) = 0
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = threadIdx.x + u * NTH, i = e / NCL, c = e % NCL;
+      if (i < LQ) {
+        *reinterpret_cast<uint4*>(Qs + ioff<NC>(i, c)) = rq[u];
+        *reinterpret_cast<uint4*>(dOs + ioff<NC>(i, c)) = rdo[u];
+        const uint32_t wa[4] = {rdo[u].x, rdo[u].y, rdo[u].z, rdo[u].w}, wb[4] = {ro[u].x, ro[u].y, ro[u].z, ro[u].w};
+        float acc = 0.f;
+#pragma unroll
+        for (int t2 = 0; t2 < 4; ++t2)
+          acc += __uint_as_float(wa[t2] << 16) * __uint_as_float(wb[t2] << 16) +
+                 __uint_as_float(wa[t2] & 0xffff0000u) * __uint_as_float(wb[t2] & 0xffff0000u);
+        scr[e] = acc;
+      }
+      if (i < LK) *reinterpret_cast<uint4*>(Ks + ioff<NC>(i, c)) = rk[u];
+    }
+    if (t < LK) msk[t] = mv;
+    __syncthreads();
+    if (t < LQ) {
+      float acc = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCL; ++c) acc += scr[t * NCL + c];
+      Ds[t] = acc;
+      Ls[t] = lv;
     }
   }
   __syncthreads();
@@ -612,7 +652,7 @@ size_t bwd_km_lds(int lq, int lk, int hd) {
   const size_t LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
   if (hd == 96) hd = 128;
   const size_t QW = LQ == 96 ? 128 : LQ;
-  return 2 * (std::max(2 * LQ * hd, LK * QW) + LK * hd) + 4 * (LK + 2 * LQ);
+  return 2 * (std::max(2 * LQ * hd, LK * QW) + LK * hd) + 4 * (LK + 2 * LQ) + 4 * LQ * (hd / 8);
 }
 
 size_t fwd_lds(int lq, int lk, int hd) {

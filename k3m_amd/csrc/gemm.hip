@@ -172,7 +172,6 @@ int launch_x6_persistent_one(const K3mGemm& g, bool t256, bool ak, bool bk, hipS
 }  // namespace
 
 int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st, bool slabs_only, bool colsum);  // gemm_bf16.hip
-int k3m_gemm_x6d_impl(const K3mGemm& g, long long pa, long long pb, hipStream_t st);       // gemm_x6d.hip
 int k3m_gemm_bf16_grouped_impl(const K3mGemm* gs, int count, hipStream_t st, bool* handled, const bool* slabs_only);
 // (the grouped problems carry their COLSUM_SLABS request as a non-null ws with splitk <= 1)
 
@@ -196,9 +195,8 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
   K3M_ARG(g.epilogue == K3M_EPI_NONE || g.epilogue == K3M_EPI_DGELU || g.bias);
   K3M_ARG((g.epilogue != K3M_EPI_BIAS_GELU && g.epilogue != K3M_EPI_DGELU) || g.aux);
   K3M_ARG(g.f32_algo == K3M_F32_SPLIT_BF16X6 || g.f32_algo == K3M_F32_MFMA_F32);
-  K3M_ARG(g.a_planes >= 0 && g.b_planes >= 0 && ((g.a_planes > 0) == (g.b_planes > 0)));
+  K3M_ARG(g.a_planes == 0 && g.b_planes == 0);   // reserved (the round-3 pre-split lab path, scripts/lab/r3)
   if (g.dtype == K3M_BF16) {
-    K3M_ARG(g.a_planes == 0);
     return k3m_gemm_bf16_impl(g, st, slabs_only, colsum);
   }
   // A: K-contiguous iff a_trans == 0; B: K-contiguous iff b_trans == 1
@@ -209,10 +207,7 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
   // tile choice: the largest tile that still fills the 256 CUs; small co-attention GEMMs
   // (2,304-8,192 rows) otherwise leave CUs idle
   int rc;
-  if (g.a_planes > 0) {   // pre-split operands (k3m_split3): the LDS-DMA x6 kernel, no other path reads planes
-    K3M_ARG(g.f32_algo == K3M_F32_SPLIT_BF16X6);
-    rc = k3m_gemm_x6d_impl(g, g.a_planes, g.b_planes, st);
-  } else if (vec && g.f32_algo == K3M_F32_SPLIT_BF16X6) {
+  if (vec && g.f32_algo == K3M_F32_SPLIT_BF16X6) {
     const int vrc = kVariant ? k3m_x6_variant_launch(g, kVariant, st) : -1;
     if (vrc >= 0) {
       rc = vrc;

@@ -157,39 +157,6 @@ def gemm(a, a_trans, b, b_trans, c, m, n, k, epi=L.EPI_NONE, bias=None, aux=None
     return c
 
 
-def split3(x, out=None):
-    """The exact three-way bf16 split of an fp32 matrix (k3m_split3): a (3, rows, cols) bf16 tensor of the
-    planes h, m, l with x = h + m + l, the pre-split operand form of gemm_planes."""
-    rows, cols = x.shape
-    if out is None:
-        out = torch.empty((3, rows, cols), dtype=torch.bfloat16, device=x.device)
-    call("k3m_split3", ptr(x), _ld(x), rows, cols, ptr(out), out.stride(1), out.stride(0), stream())
-    return out
-
-
-def gemm_planes(ap, a_trans, bp, b_trans, c, m, n, k, epi=L.EPI_NONE, bias=None, aux=None, alpha=1.0, beta=0.0,
-                splitk=1, ws=None):
-    """gemm() of fp32 numbers given pre-split (split3 planes, (3, rows, cols) bf16): the LDS-DMA bf16x6 kernel,
-    bit-identical to splitting in the kernel."""
-    assert ap.dim() == 3 and bp.dim() == 3 and ap.dtype == torch.bfloat16 and bp.dtype == torch.bfloat16
-    g = L.K3mGemm()
-    g.f32_algo = L.F32_SPLIT_BF16X6
-    g.m, g.n, g.k = m, n, k
-    g.a_trans, g.b_trans = a_trans, b_trans
-    g.epilogue, g.dtype, g.splitk, g.c_dtype = epi, L.F32, splitk, dt(c)
-    g.lda, g.ldb, g.ldc = ap.stride(1), bp.stride(1), _ld(c)
-    g.ldaux = _ld(aux) if aux is not None else 0
-    g.a, g.b, g.c = ptr(ap), ptr(bp), ptr(c)
-    g.bias, g.aux, g.ws = ptr(bias), ptr(aux), ptr(ws)
-    g.alpha, g.beta = alpha, beta
-    g.a_planes, g.b_planes = ap.stride(0), bp.stride(0)
-    if _grouper is not None:
-        _grouper.pending.append((g, (ap, bp, c, bias, aux, ws)))
-        return c
-    call("k3m_gemm", L.C.byref(g), stream())
-    return c
-
-
 def linear(x, W, b=None, out=None, epi=None, aux=None, alpha=1.0, beta=0.0, out_dtype=None):
     """out = x . W^T (+ b) with epilogue; x [M,K] (row view), W [N,K]."""
     M, K = x.shape
@@ -470,7 +437,7 @@ def flash_fits(lq, lk, hd):
     fwd = 2 * (LQ * h + 2 * LK * h) + 4 * LK
     if FLASH_BWD_KM:
         QW = 128 if LQ == 96 else LQ
-        bwd = 2 * (max(2 * LQ * h, LK * QW) + LK * h) + 4 * (LK + 2 * LQ)
+        bwd = 2 * (max(2 * LQ * h, LK * QW) + LK * h) + 4 * (LK + 2 * LQ) + 4 * LQ * (h // 8)
     else:
         PW = 128 if LK == 96 else LK
         bwd = 2 * (2 * LQ * h + 2 * LK * h + 2 * LQ * PW) + 4 * (LK + 2 * LQ)

@@ -1,5 +1,6 @@
 """Counter table of one kernel from scripts/pmc_gemm.sh passes: mean per dispatch + derived rates.
-usage: pmc_table.py <tag> <kernel-name substring> [flops_per_dispatch] [algorithmic_bytes]"""
+usage: pmc_table.py <tag> <kernel-name substring> [flops_per_dispatch] [algorithmic_bytes] [M,N,K]
+(bench.py reads traffic_bytes of the newest record whose shape and full kernel name match the kernel it runs)"""
 import csv
 import glob
 import json
@@ -9,18 +10,22 @@ from collections import defaultdict
 tag, sub = sys.argv[1], sys.argv[2]
 flops = float(sys.argv[3]) if len(sys.argv) > 3 else None
 alg_bytes = float(sys.argv[4]) if len(sys.argv) > 4 else None
+shape = [int(x) for x in sys.argv[5].split(",")] if len(sys.argv) > 5 else None
 vals = defaultdict(list)
+names = set()
 durs = []
 for path in sorted(glob.glob("gpurun_out/pmc_%s_*/**/*counter_collection.csv" % tag, recursive=True)):
     for r in csv.DictReader(open(path)):
         if sub in r["Kernel_Name"]:
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            names.add(r["Kernel_Name"])
 for path in sorted(glob.glob("gpurun_out/pmc_%s_*/**/*kernel_trace.csv" % tag, recursive=True)):
     for r in csv.DictReader(open(path)):
         if sub in r["Kernel_Name"]:
             durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 m = {k: sum(v) / len(v) for k, v in vals.items()}
-out = {"tag": tag, "kernel": sub, "counters_mean_per_dispatch": m,
+out = {"tag": tag, "kernel": sorted(names)[0] if len(names) == 1 else sub, "kernel_names": sorted(names),
+       "shape": shape, "counters_mean_per_dispatch": m,
        "dispatches": {k: len(v) for k, v in vals.items()}}
 if durs:
     # profiled dispatches only (clocks differ from un-profiled runs: MI355X_MICROARCH.md DVFS item 2)

@@ -236,46 +236,3 @@ def test_dgelu_colsum_slabs(dev, dtype, m, n, k):
     # per 32-row group
     grp = torch.nn.functional.pad(c.double(), (0, 0, 0, ns * 32 - m)).view(ns, 32, n).sum(1)
     assert float((slabs.double() - grp).abs().max()) <= 1e-5 * float(grp.abs().max()) + 1e-6
-
-
-def test_split3_exact(dev):
-    """k3m_split3: h = rne_bf16(x), and h + m + l == x exactly (including tiny and large magnitudes)."""
-    from k3m_amd import ops
-    g = torch.Generator(device="cpu").manual_seed(5)
-    x = (torch.randn(300, 776, generator=g) * torch.logspace(-20, 20, 776).float()).to(dev)
-    p = ops.split3(x)
-    torch.cuda.synchronize()
-    assert torch.equal(p[0], x.to(torch.bfloat16))
-    s = p[0].double() + p[1].double() + p[2].double()
-    assert torch.equal(s, x.double())
-
-
-@pytest.mark.parametrize("m,n,k,at,bt,epi,splitk", [
-    (4096, 3072, 768, 0, 1, 2, 1),     # forward + bias + GELU (pre-activation aux)
-    (1000, 904, 784, 0, 1, 1, 1),      # ragged M / N edges, forward + bias
-    (4096, 768, 3072, 0, 0, 0, 1),     # input gradient (B MN-contiguous)
-    (2000, 3072, 768, 0, 0, 3, 1),     # input gradient with dGELU
-    (3072, 768, 8192, 1, 0, 0, 4),     # weight gradient, split-K, beta = 1
-    (2304, 1000, 512, 1, 1, 4, 1),     # A MN-contiguous, B K-contiguous, bias + sigmoid
-])
-def test_presplit_planes_bit_identical(dev, m, n, k, at, bt, epi, splitk):
-    """K3mGemm.a_planes / b_planes: the LDS-DMA kernel on pre-split operands (gemm_x6d.hip) gives exactly the
-    in-kernel-split bf16x6 result (same products, same order per accumulator, same epilogue)."""
-    from k3m_amd import ops
-    g = torch.Generator(device="cpu").manual_seed(m + n + k)
-    a = (torch.randn(k, m, generator=g) if at else torch.randn(m, k, generator=g)).to(dev)
-    b = (torch.randn(n, k, generator=g) if bt else torch.randn(k, n, generator=g)).mul_(0.05).to(dev)
-    bias = torch.randn(n, generator=g).to(dev) if epi in (1, 2, 4) else None
-    aux_in = torch.randn(m, n, generator=g).to(dev) if epi == 3 else None
-    beta = 1.0 if splitk > 1 else 0.0
-    c0 = torch.randn(m, n, generator=g).to(dev)
-    c1 = c0.clone()
-    aux0 = torch.empty(m, n, device=dev) if epi == 2 else aux_in
-    aux1 = torch.empty(m, n, device=dev) if epi == 2 else aux_in
-    ws = torch.empty(splitk * m * n, device=dev) if splitk > 1 else None
-    ops.gemm(a, at, b, bt, c0, m, n, k, epi, bias, aux0, 1.0, beta, splitk, ws)
-    ops.gemm_planes(ops.split3(a), at, ops.split3(b), bt, c1, m, n, k, epi, bias, aux1, 1.0, beta, splitk, ws)
-    torch.cuda.synchronize()
-    assert torch.equal(c0, c1)
-    if epi == 2:
-        assert torch.equal(aux0, aux1)
