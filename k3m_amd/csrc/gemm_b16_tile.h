@@ -417,7 +417,7 @@ struct NoHookB {
 // persistent walk issues the next tile's first LDS-DMA there; the staging image then must not overlap stage 0).
 template <int TBM, int TBN, int WM, int WN, int EPI, typename CT, typename AccT, class Hook = NoHookB>
 __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint16_t* smem_u16, const AccT& acc,
-                                         int slice, Hook hook = Hook()) {
+                                         int slice, Hook hook = Hook(), bool nostore = false) {
   using S = Shape<TBM, TBN, WM, WN>;
   constexpr int WNC = TBN / WN, WS = WNC + 8, LPR = WNC / 8, RPP = 64 / LPR, NPS = 32 / RPP, NG = TBM / WM / 32;
   constexpr int RING = sizeof(CT) == 2 ? 2 : 1;   // passes the per-pass loads run ahead (register budget)
@@ -490,8 +490,13 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint1
           if (q + RING < NQ) issue(q + RING, slot);
           float o[8], pa[8];
           epi_math8<EPI>(v, bb, ax, old, alpha, beta, OLD, o, pa);
-          store8(C + row * ldc + col, o);
-          if constexpr (EPI == K3M_EPI_BIAS_GELU) store8(aux + row * g.ldaux + col, pa);
+          if (nostore) {   // lab timing (K3M_B16_LAB bit 0): the math stays live, nothing is written
+#pragma unroll
+            for (int e = 0; e < 8; ++e) asm volatile("" ::"v"(o[e]), "v"(pa[e]));
+          } else {
+            store8(C + row * ldc + col, o);
+            if constexpr (EPI == K3M_EPI_BIAS_GELU) store8(aux + row * g.ldaux + col, pa);
+          }
           if constexpr (CSUM) {
             if (cws)
 #pragma unroll
@@ -596,6 +601,8 @@ struct GemmGroup {
   K3mGemm g[GROUP_MAX];
   int start[GROUP_MAX + 1];
   int count;
+  int lab;       // lab knob K3M_B16_LAB (timing experiments only): bit 0 = no C / aux stores, bit 1 = staggered start
+  int stagger;   // bit 1: workgroup b waits (b & 3) * stagger ticks of the 100 MHz clock before its first tile
 };
 
 // one output tile on MF x MF x (512 / MF) MFMAs (MF = 16 or 32)
@@ -676,6 +683,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_persist_kernel(GemmGroup
   const int total = grp.start[grp.count];
   int u = blockIdx.x;
   if (u >= total) return;
+  if (grp.lab & 2) {   // lab: staggered start (bounded wait on the 100 MHz real-time clock)
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t until = t0 + (uint64_t)(blockIdx.x & 3) * (uint64_t)grp.stagger;
+    while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(8);
+  }
+  const bool nostore = (grp.lab & 1) != 0;
   PUnit<TBM, TBN, WM, WN> cur;
   cur.decode(grp, u);
   bool pre = false;
@@ -706,10 +719,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_persist_kernel(GemmGroup
           lb.issue(smem + TBM * BK);
         }
       };
-      epilogue<TBM, TBN, WM, WN, EPI, CT>(g, cur.m0, cur.n0, smem + EOFF, acc, cur.slice, hook);
+      epilogue<TBM, TBN, WM, WN, EPI, CT>(g, cur.m0, cur.n0, smem + EOFF, acc, cur.slice, hook, nostore);
       next_pre = issue;
     } else {
-      epilogue<TBM, TBN, WM, WN, EPI, CT>(g, cur.m0, cur.n0, smem, acc, cur.slice);
+      epilogue<TBM, TBN, WM, WN, EPI, CT>(g, cur.m0, cur.n0, smem, acc, cur.slice, NoHookB(), nostore);
     }
     if (!more) break;
     u = nu;

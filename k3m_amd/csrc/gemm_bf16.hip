@@ -475,8 +475,16 @@ int b16_cus() {
 // +0.1 % on the bf16 step, within noise: off, profiles/r3_ab_b16_persist.txt)
 const bool kB16Prefetch = k3m_env_flag("K3M_B16_PREFETCH", false);
 
+// timing-only lab knobs of the persistent walk (never set in product runs): K3M_B16_LAB bit 0 = skip the C / aux
+// stores, bit 1 = staggered start of K3M_B16_STAGGER ticks (10 ns) per workgroup group (b & 3)
+const int kB16Lab = k3m_env_int("K3M_B16_LAB", 0);
+const int kB16Stagger = k3m_env_int("K3M_B16_STAGGER", 500);
+
 template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF>
-void persist_launch(const k3m_b16::GemmGroup& grp, hipStream_t st) {
+void persist_launch(const k3m_b16::GemmGroup& grp_in, hipStream_t st) {
+  k3m_b16::GemmGroup grp = grp_in;
+  grp.lab = kB16Lab;
+  grp.stagger = kB16Stagger;
   const int total = grp.start[grp.count];
   const int nblk = total < b16_cus() ? total : b16_cus();
   if (kB16Prefetch)

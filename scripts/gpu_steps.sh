@@ -65,6 +65,8 @@ for s in "$@"; do
     rccl) step rccl 900 python -u -m pytest tests/test_gpu_rccl.py -v -s --timeout 300 --timeout-method thread ;;
     standin) step standin 300 python -u -m pytest tests/test_gpu_dropin.py -q --timeout 200 --timeout-method thread ;;
     abkm) step abkm 900 scripts/ab_env.sh K3M_FLASH_BWD_KM "0 1" 3 --config 3 --steps 10 --warmup 4 ;;
+    b16lab) for r in 1 2; do for lab in 0 1 2 3; do
+              K3M_B16_LAB=$lab step b16lab_${lab}_$r 300 python scripts/gemm_bench.py all 20 bf16; done; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
