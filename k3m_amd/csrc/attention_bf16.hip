@@ -90,8 +90,9 @@ __device__ __forceinline__ void stage(uint16_t* img, const uint16_t* __restrict_
   for (int u = 0; u < U; ++u) {
     const int e = threadIdx.x + u * NT;
     const int i = e / NC, c = e % NC;
-    r[u] = make_uint4(0u, 0u, 0u, 0u);
-    if (i < nvalid) r[u] = *reinterpret_cast<const uint4*>(src + (row0 + i) * ld + coff + 8 * c);
+    // unconditional load from a clamped row, zeroed after it (no per-element branch + vmcnt(0))
+    const uint4 x = *reinterpret_cast<const uint4*>(src + (row0 + min(i, nvalid - 1)) * ld + coff + 8 * c);
+    r[u] = i < nvalid ? x : make_uint4(0u, 0u, 0u, 0u);
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -131,12 +132,17 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __rest
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int e = threadIdx.x + u * NT, i = e / NCL, c = e % NCL;
+      // unconditional loads from clamped rows, zeroed after the load: a load under a per-element runtime
+      // condition makes hipcc branch around it with a vmcnt(0) inside (every load one round trip)
       const uint4 z = make_uint4(0u, 0u, 0u, 0u);
       const bool qv = i < lq, kv = i < lk;
-      const long long qo = qrow0 + (qv ? i : 0), ko = krow0 + (kv ? i : 0);
-      rq[u] = qv ? *reinterpret_cast<const uint4*>(q + qo * ldq + hoff + 8 * c) : z;
-      rk[u] = kv ? *reinterpret_cast<const uint4*>(k + ko * ldk + hoff + 8 * c) : z;
-      rv[u] = kv ? *reinterpret_cast<const uint4*>(v + ko * ldv + hoff + 8 * c) : z;
+      const long long qo = qrow0 + min(i, lq - 1), ko = krow0 + min(i, lk - 1);
+      const uint4 a = *reinterpret_cast<const uint4*>(q + qo * ldq + hoff + 8 * c);
+      const uint4 b = *reinterpret_cast<const uint4*>(k + ko * ldk + hoff + 8 * c);
+      const uint4 d = *reinterpret_cast<const uint4*>(v + ko * ldv + hoff + 8 * c);
+      rq[u] = qv ? a : z;
+      rk[u] = kv ? b : z;
+      rv[u] = kv ? d : z;
     }
     const int t = threadIdx.x;
     float mv = 0.f;
@@ -428,28 +434,6 @@ __device__ __forceinline__ int ioff_n(int nc, int r, int c) {
   return nc == 4 ? ioff<4>(r, c) : nc == 8 ? ioff<8>(r, c) : ioff<16>(r, c);
 }
 
-// rows [row0, row0 + nrows) x [coff, coff + 8 NCS) of a bf16 matrix -> image with NCI chunks per row
-// (rows >= nvalid zero), NTH threads, every load issued before the LDS writes
-template <int NCS, int NCI, int NTH>
-__device__ __forceinline__ void stage_n(uint16_t* img, const uint16_t* __restrict__ src, long long row0, long long ld,
-                                        int coff, int nrows, int nvalid) {
-  constexpr int U = (MAXL * NCS + NTH - 1) / NTH;
-  uint4 r[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int e = threadIdx.x + u * NTH;
-    const int i = e / NCS, c = e % NCS;
-    r[u] = make_uint4(0u, 0u, 0u, 0u);
-    if (i < nvalid) r[u] = *reinterpret_cast<const uint4*>(src + (row0 + i) * ld + coff + 8 * c);
-  }
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int e = threadIdx.x + u * NTH;
-    const int i = e / NCS, c = e % NCS;
-    if (i < nrows) *reinterpret_cast<uint4*>(img + ioff<NCI>(i, c)) = r[u];
-  }
-}
-
 template <int HD>
 constexpr int km_occupancy() { return HD == 64 ? 2 : 1; }
 
@@ -490,14 +474,15 @@ __global__ __launch_bounds__(NW * 64, km_occupancy<HD>()) void flash_bwd_km_kern
   bf16x8 kf[KS], vf[KS];
   {
     const bool ok = kw && j < lk;
-    const uint16_t* kp = k + (krow0 + (ok ? j : 0)) * ldk + hoff + 8 * kl;
-    const uint16_t* vp = v + (krow0 + (ok ? j : 0)) * ldv + hoff + 8 * kl;
+    const uint16_t* kp = k + (krow0 + min(j, lk - 1)) * ldk + hoff + 8 * kl;
+    const uint16_t* vp = v + (krow0 + min(j, lk - 1)) * ldv + hoff + 8 * kl;
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      const uint4 a = ok ? *reinterpret_cast<const uint4*>(kp + 16 * ks) : make_uint4(0u, 0u, 0u, 0u);
-      const uint4 b = ok ? *reinterpret_cast<const uint4*>(vp + 16 * ks) : make_uint4(0u, 0u, 0u, 0u);
-      kf[ks] = __builtin_bit_cast(bf16x8, a);
-      vf[ks] = __builtin_bit_cast(bf16x8, b);
+      const uint4 a = *reinterpret_cast<const uint4*>(kp + 16 * ks);
+      const uint4 b = *reinterpret_cast<const uint4*>(vp + 16 * ks);
+      kf[ks] = __builtin_bit_cast(bf16x8, ok ? a : z);
+      vf[ks] = __builtin_bit_cast(bf16x8, ok ? b : z);
     }
   }
   {
@@ -509,13 +494,18 @@ __global__ __launch_bounds__(NW * 64, km_occupancy<HD>()) void flash_bwd_km_kern
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int e = threadIdx.x + u * NTH, i = e / NCL, c = e % NCL;
+      // unconditional loads from clamped rows, zeroed after the load (see flash_fwd_kernel)
       const uint4 z = make_uint4(0u, 0u, 0u, 0u);
       const bool qv = i < lq, kv = i < lk;
-      const long long qo = (qrow0 + (qv ? i : 0)), ko = (krow0 + (kv ? i : 0));
-      rq[u] = qv ? *reinterpret_cast<const uint4*>(q + qo * ldq + hoff + 8 * c) : z;
-      rdo[u] = qv ? *reinterpret_cast<const uint4*>(dctx + qo * ldc + hoff + 8 * c) : z;
-      ro[u] = qv ? *reinterpret_cast<const uint4*>(o + qo * ldo + hoff + 8 * c) : z;
-      rk[u] = kv ? *reinterpret_cast<const uint4*>(k + ko * ldk + hoff + 8 * c) : z;
+      const long long qo = qrow0 + min(i, lq - 1), ko = krow0 + min(i, lk - 1);
+      const uint4 a = *reinterpret_cast<const uint4*>(q + qo * ldq + hoff + 8 * c);
+      const uint4 b = *reinterpret_cast<const uint4*>(dctx + qo * ldc + hoff + 8 * c);
+      const uint4 d = *reinterpret_cast<const uint4*>(o + qo * ldo + hoff + 8 * c);
+      const uint4 f = *reinterpret_cast<const uint4*>(k + ko * ldk + hoff + 8 * c);
+      rq[u] = qv ? a : z;
+      rdo[u] = qv ? b : z;
+      ro[u] = qv ? d : z;
+      rk[u] = kv ? f : z;
     }
     float mv = 0.f, lv = 0.f;
     const int t = threadIdx.x;
