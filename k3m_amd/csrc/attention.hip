@@ -484,6 +484,15 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
   ATT_STAMP_END(5);
 }
 
+// x where ok, zeros elsewhere, per 32-bit word: a whole-float4 ?: select under a per-lane condition was lowered
+// to a scratch store + indexed reload (or a branch + vmcnt(0) around the load); loads stay unconditional from
+// clamped (valid) addresses
+__device__ __forceinline__ float4 keep4(bool ok, float4 x) {
+  const uint32_t m = ok ? 0xffffffffu : 0u;
+  return make_float4(__uint_as_float(__float_as_uint(x.x) & m), __uint_as_float(__float_as_uint(x.y) & m),
+                     __uint_as_float(__float_as_uint(x.z) & m), __uint_as_float(__float_as_uint(x.w) & m));
+}
+
 // ------------------------------------------------------------------ forward, probabilities in registers
 // fp32, lq, lk <= 128, K and V of the head in LDS (<= 80 KB: two or more workgroups per CU).  One
 // wave per 32-query block, the queries on the MFMA lanes:
@@ -529,9 +538,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_reg_kernel(const float* __res
     for (int u = 0; u < U; ++u) {
       const int e = threadIdx.x + u * NTH, j = e / NCH, c = e % NCH;
       const bool ok = e < LK * NCH && j < lk;
-      const long long row = krow0 + (ok ? j : 0);
-      kc[u] = ok ? *reinterpret_cast<const float4*>(k + row * ldk + hoff + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
-      vc[u] = ok ? *reinterpret_cast<const float4*>(v + row * ldv + hoff + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const long long row = krow0 + min(j, lk - 1);
+      kc[u] = keep4(ok, *reinterpret_cast<const float4*>(k + row * ldk + hoff + 4 * c));
+      vc[u] = keep4(ok, *reinterpret_cast<const float4*>(v + row * ldv + hoff + 4 * c));
     }
     float mv = 0.f;
     if (threadIdx.x < LK && kmask) mv = kmask[krow0 + min((int)threadIdx.x, lk - 1)];
@@ -552,7 +561,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_reg_kernel(const float* __res
     const float* src = q + (qrow0 + (ok ? qi : 0)) * ldq + hoff + kl * HH;
 #pragma unroll
     for (int c = 0; c < HH / 4; ++c) {
-      const float4 t = ok ? *reinterpret_cast<const float4*>(src + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 t = keep4(ok, *reinterpret_cast<const float4*>(src + 4 * c));
       qr[4 * c] = t.x * sl;
       qr[4 * c + 1] = t.y * sl;
       qr[4 * c + 2] = t.z * sl;
@@ -763,10 +772,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x6_kernel(const float* __rest
       const int e = threadIdx.x + u * NTH;
       const int j = e / NCH, c = e % NCH;                 // K: row-major chunks (coalesced)
       const bool ok = e < LK * NCH && j < lk;
-      kc[u] = ok ? *reinterpret_cast<const float4*>(k + (krow0 + j) * ldk + hoff + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      kc[u] = keep4(ok, *reinterpret_cast<const float4*>(k + (krow0 + min(j, lk - 1)) * ldk + hoff + 4 * (c % NCH)));
       const int jv = e % LK, cv = e / LK;                 // V: 64 consecutive keys per wave instruction
       const bool okv = e < LK * NCH && jv < lk;
-      vc[u] = okv ? *reinterpret_cast<const float4*>(v + (krow0 + jv) * ldv + hoff + 4 * cv) : make_float4(0.f, 0.f, 0.f, 0.f);
+      vc[u] = keep4(okv, *reinterpret_cast<const float4*>(v + (krow0 + min(jv, lk - 1)) * ldv + hoff +
+                                                           4 * min(cv, NCH - 1)));
     }
     float mv = 0.f;
     if (threadIdx.x < LK && kmask) mv = kmask[krow0 + min((int)threadIdx.x, lk - 1)];
@@ -794,7 +804,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x6_kernel(const float* __rest
     const float* src = q + (qrow0 + (ok ? qi : 0)) * ldq + hoff + kl * HH;
 #pragma unroll
     for (int c = 0; c < HH / 4; ++c) {
-      const float4 t = ok ? *reinterpret_cast<const float4*>(src + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 t = keep4(ok, *reinterpret_cast<const float4*>(src + 4 * c));
       qr[4 * c] = t.x * sl;
       qr[4 * c + 1] = t.y * sl;
       qr[4 * c + 2] = t.z * sl;
@@ -1004,8 +1014,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_reg_kernel(
       const int e = threadIdx.x + u * NTH, i = e / NCH, c = e % NCH;
       const bool ok = e < LQ * NCH && i < lq;
       const long long row = qrow0 + (ok ? i : 0);
-      cdo[u] = ok ? *reinterpret_cast<const float4*>(dctx + row * ldc + hoff + 4 * c) : z4;
-      co[u] = ok ? *reinterpret_cast<const float4*>(o + row * ldo + hoff + 4 * c) : z4;
+      cdo[u] = keep4(ok, *reinterpret_cast<const float4*>(dctx + row * ldc + hoff + 4 * c));
+      co[u] = keep4(ok, *reinterpret_cast<const float4*>(o + row * ldo + hoff + 4 * c));
     }
 #pragma unroll
     for (int u = 0; u < UQ; ++u) {
@@ -1024,7 +1034,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_reg_kernel(
     const float* src = v + (krow0 + (ok ? key : 0)) * ldv + hoff + kl * HH;
 #pragma unroll
     for (int c = 0; c < HH / 4; ++c) {
-      const float4 t = ok ? *reinterpret_cast<const float4*>(src + 4 * c) : z4;
+      const float4 t = keep4(ok, *reinterpret_cast<const float4*>(src + 4 * c));
       vr[4 * c] = t.x;
       vr[4 * c + 1] = t.y;
       vr[4 * c + 2] = t.z;

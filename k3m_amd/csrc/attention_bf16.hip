@@ -32,6 +32,13 @@ typedef short short4v __attribute__((ext_vector_type(4)));
 typedef short short8v __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) short4v lds_short4v;
 
+// keep x where ok, zero elsewhere, per 32-bit word: a ?: select of a whole uint4 was lowered to a
+// scratch-memory store + indexed reload of both candidates
+__device__ __forceinline__ uint4 keep_if(bool ok, uint4 x) {
+  const uint32_t m = ok ? 0xffffffffu : 0u;
+  return make_uint4(x.x & m, x.y & m, x.z & m, x.w & m);
+}
+
 // element offset of chunk c (8 bf16) of row r in an image whose rows hold NC chunks
 template <int NC>
 __device__ __forceinline__ int ioff(int r, int c) {
@@ -92,7 +99,7 @@ __device__ __forceinline__ void stage(uint16_t* img, const uint16_t* __restrict_
     const int i = e / NC, c = e % NC;
     // unconditional load from a clamped row, zeroed after it (no per-element branch + vmcnt(0))
     const uint4 x = *reinterpret_cast<const uint4*>(src + (row0 + min(i, nvalid - 1)) * ld + coff + 8 * c);
-    r[u] = i < nvalid ? x : make_uint4(0u, 0u, 0u, 0u);
+    r[u] = keep_if(i < nvalid, x);
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -134,15 +141,14 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __rest
       const int e = threadIdx.x + u * NT, i = e / NCL, c = e % NCL;
       // unconditional loads from clamped rows, zeroed after the load: a load under a per-element runtime
       // condition makes hipcc branch around it with a vmcnt(0) inside (every load one round trip)
-      const uint4 z = make_uint4(0u, 0u, 0u, 0u);
       const bool qv = i < lq, kv = i < lk;
       const long long qo = qrow0 + min(i, lq - 1), ko = krow0 + min(i, lk - 1);
       const uint4 a = *reinterpret_cast<const uint4*>(q + qo * ldq + hoff + 8 * c);
       const uint4 b = *reinterpret_cast<const uint4*>(k + ko * ldk + hoff + 8 * c);
       const uint4 d = *reinterpret_cast<const uint4*>(v + ko * ldv + hoff + 8 * c);
-      rq[u] = qv ? a : z;
-      rk[u] = kv ? b : z;
-      rv[u] = kv ? d : z;
+      rq[u] = keep_if(qv, a);
+      rk[u] = keep_if(kv, b);
+      rv[u] = keep_if(kv, d);
     }
     const int t = threadIdx.x;
     float mv = 0.f;
@@ -476,13 +482,12 @@ __global__ __launch_bounds__(NW * 64, km_occupancy<HD>()) void flash_bwd_km_kern
     const bool ok = kw && j < lk;
     const uint16_t* kp = k + (krow0 + min(j, lk - 1)) * ldk + hoff + 8 * kl;
     const uint16_t* vp = v + (krow0 + min(j, lk - 1)) * ldv + hoff + 8 * kl;
-    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const uint4 a = *reinterpret_cast<const uint4*>(kp + 16 * ks);
       const uint4 b = *reinterpret_cast<const uint4*>(vp + 16 * ks);
-      kf[ks] = __builtin_bit_cast(bf16x8, ok ? a : z);
-      vf[ks] = __builtin_bit_cast(bf16x8, ok ? b : z);
+      kf[ks] = __builtin_bit_cast(bf16x8, keep_if(ok, a));
+      vf[ks] = __builtin_bit_cast(bf16x8, keep_if(ok, b));
     }
   }
   {
@@ -495,17 +500,16 @@ __global__ __launch_bounds__(NW * 64, km_occupancy<HD>()) void flash_bwd_km_kern
     for (int u = 0; u < U; ++u) {
       const int e = threadIdx.x + u * NTH, i = e / NCL, c = e % NCL;
       // unconditional loads from clamped rows, zeroed after the load (see flash_fwd_kernel)
-      const uint4 z = make_uint4(0u, 0u, 0u, 0u);
       const bool qv = i < lq, kv = i < lk;
       const long long qo = qrow0 + min(i, lq - 1), ko = krow0 + min(i, lk - 1);
       const uint4 a = *reinterpret_cast<const uint4*>(q + qo * ldq + hoff + 8 * c);
       const uint4 b = *reinterpret_cast<const uint4*>(dctx + qo * ldc + hoff + 8 * c);
       const uint4 d = *reinterpret_cast<const uint4*>(o + qo * ldo + hoff + 8 * c);
       const uint4 f = *reinterpret_cast<const uint4*>(k + ko * ldk + hoff + 8 * c);
-      rq[u] = qv ? a : z;
-      rdo[u] = qv ? b : z;
-      ro[u] = qv ? d : z;
-      rk[u] = kv ? f : z;
+      rq[u] = keep_if(qv, a);
+      rdo[u] = keep_if(qv, b);
+      ro[u] = keep_if(qv, d);
+      rk[u] = keep_if(kv, f);
     }
     float mv = 0.f, lv = 0.f;
     const int t = threadIdx.x;

@@ -44,7 +44,9 @@ __device__ __forceinline__ floatx4 round4(floatx4 v) {
 }
 
 // ------------------------------------------------------------------ LayerNorm forward
-template <typename T>
+// NV = cols / 256 is a template parameter: with a runtime chunk count every load sat under a per-element
+// condition, which hipcc compiles to a branch with a vmcnt(0) inside (each load its own round trip)
+template <typename T, int NV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      T* __restrict__ y, T* __restrict__ xhat, float* __restrict__ rstd,
@@ -53,20 +55,25 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
-  const int nv = cols >> 8;  // float4 chunks per lane
+  constexpr int nv = NV;  // float4 chunks per lane
   const long long base = (long long)row * cols;
-  floatx4 v[MAXV];
+  floatx4 v[MAXV], r[MAXV];
+  const T* rp = res ? res : x;   // every load unconditional and issued before the arithmetic
+#pragma unroll
+  for (int j = 0; j < nv; ++j) v[j] = ld4<T>(x + base + (lane + 64 * j) * 4);
+#pragma unroll
+  for (int j = 0; j < nv; ++j) r[j] = ld4<T>(rp + base + (lane + 64 * j) * 4);
   float sum = 0.f;
 #pragma unroll
   for (int j = 0; j < MAXV; ++j) {
     if (j < nv) {
       const int c = (lane + 64 * j) * 4;
-      floatx4 a = ld4<T>(x + base + c);
+      floatx4 a = v[j];
       if (p_in > 0.f) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) a[q] *= k3m_dropout_scale(seed, off_in + base + c + q, p_in);
       }
-      if (res) a += ld4<T>(res + base + c);
+      if (res) a += r[j];
       v[j] = a;
       sum += a[0] + a[1] + a[2] + a[3];
     }
@@ -132,10 +139,20 @@ __global__ __launch_bounds__(256) void slab_batch_kernel(SlabJobs jobs) {
     const int c4 = (((int)blockIdx.x - jobs.start[j]) * 256 + (int)threadIdx.x) * 4;
     if (c4 >= cols) return;
     const float* src = jobs.ws[j] + c4;
-    floatx4 acc = *reinterpret_cast<const floatx4*>(src);
-    for (int k = 1; k < nslab; ++k) acc += *reinterpret_cast<const floatx4*>(src + (long long)k * cols);
     floatx4* o = reinterpret_cast<floatx4*>(jobs.out[j] + c4);
-    *o = jobs.accumulate[j] ? *o + acc : acc;
+    const floatx4 old = *o;   // issued first, used last
+    floatx4 acc = *reinterpret_cast<const floatx4*>(src);
+    // slabs summed in order 0..nslab-1 (deterministic), loads issued 8 slabs ahead of the adds
+    int k = 1;
+    for (; k + 8 <= nslab; k += 8) {
+      floatx4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const floatx4*>(src + (long long)(k + u) * cols);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += t[u];
+    }
+    for (; k < nslab; ++k) acc += *reinterpret_cast<const floatx4*>(src + (long long)k * cols);
+    *o = jobs.accumulate[j] ? old + acc : acc;
     return;
   }
   const int cx = threadIdx.x & 63, ph = threadIdx.x >> 6;
@@ -163,7 +180,7 @@ __global__ __launch_bounds__(256) void slab_batch_kernel(SlabJobs jobs) {
 // ------------------------------------------------------------------ LayerNorm backward
 constexpr int LN_BWD_BLOCKS = K3M_LN_BWD_SLABS;
 
-template <typename T>
+template <typename T, int NV>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ xhat,
                                                      const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                      T* __restrict__ dres, T* __restrict__ dx, float* __restrict__ ws,
@@ -172,8 +189,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   // column partials of dgamma, dbeta and (want_sum) sum(dx): per wave in registers, then one
   // [3][cols] slab per block through LDS (summed by slab_batch_kernel)
   __shared__ float red[4][1024];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int nv = cols >> 8;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  constexpr int nv = NV;
+  floatx4 gm[MAXV];
+#pragma unroll
+  for (int j = 0; j < nv; ++j) gm[j] = *reinterpret_cast<const floatx4*>(gamma + (lane + 64 * j) * 4);
   floatx4 pg[MAXV], pb[MAXV], px[MAXV];
 #pragma unroll
   for (int j = 0; j < MAXV; ++j) {
@@ -185,24 +205,24 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   // (one row at a time left this HBM-bound kernel at ~0.44 of the bandwidth roofline)
   const int S = gridDim.x * 4;
   for (int row0 = blockIdx.x * 4 + w; row0 < rows; row0 += 2 * S) {
-    floatx4 dyl[2][MAXV], xh[2][MAXV];
+    floatx4 dyl[2][MAXV], xh[2][MAXV], rr[2][MAXV];
     float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+    const T* rsrc = acc_res ? dres : dy;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
+      // unconditional loads from a clamped row, zeroed after the load for a row past the end
       const int row = row0 + u * S;
-      const long long base = (long long)row * cols;
+      const bool ok = row < rows;
+      const long long base = (long long)min(row, rows - 1) * cols;
 #pragma unroll
-      for (int j = 0; j < MAXV; ++j)
-        if (j < nv) {
-          const int c = (lane + 64 * j) * 4;
-          if (row < rows) {
-            dyl[u][j] = ld4<T>(dy + base + c);
-            xh[u][j] = ld4<T>(xhat + base + c);
-          } else {
-            dyl[u][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-            xh[u][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-          }
-        }
+      for (int j = 0; j < nv; ++j) {
+        const int c = (lane + 64 * j) * 4;
+        const floatx4 z = floatx4{0.f, 0.f, 0.f, 0.f};
+        const floatx4 a = ld4<T>(dy + base + c), b = ld4<T>(xhat + base + c);
+        rr[u][j] = ld4<T>(rsrc + base + c);
+        dyl[u][j] = ok ? a : z;
+        xh[u][j] = ok ? b : z;
+      }
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -220,8 +240,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
           const floatx4 xv = xh[u][j];
           pg[j] += d * xv;     // rows past the end hold zeros: they add nothing
           pb[j] += d;
-          const floatx4 g = *reinterpret_cast<const floatx4*>(gamma + c);
-          const floatx4 dxh = d * g;
+          const floatx4 dxh = d * gm[j];
           s1[u] += dxh[0] + dxh[1] + dxh[2] + dxh[3];
           s2[u] += dxh[0] * xv[0] + dxh[1] * xv[1] + dxh[2] * xv[2] + dxh[3] * xv[3];
         }
@@ -237,10 +256,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
       for (int j = 0; j < MAXV; ++j)
         if (j < nv) {
           const int c = (lane + 64 * j) * 4;
-          const floatx4 g = *reinterpret_cast<const floatx4*>(gamma + c);
-          floatx4 ds = (dyl[u][j] * g - m1 - xh[u][j] * m2) * rs;
+          floatx4 ds = (dyl[u][j] * gm[j] - m1 - xh[u][j] * m2) * rs;
           floatx4 dr = ds;
-          if (acc_res) dr += ld4<T>(dres + base + c);
+          if (acc_res) dr += rr[u][j];
           st4<T>(dres + base + c, dr);
           if (dx != dres) {
             if (p_in > 0.f) {
@@ -309,6 +327,7 @@ __device__ __forceinline__ float half_sum(float v) {   // over the 32 lanes of a
   return v;
 }
 
+template <int NV>
 __global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
                                                           bf16_t* __restrict__ y, bf16_t* __restrict__ xhat,
@@ -318,19 +337,16 @@ __global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const bf16_t* __restri
   const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
   const int l = threadIdx.x & 31;
   if (row >= rows) return;   // half-wave uniform; the shuffles below stay inside the half
-  const int nv = cols >> 8;
+  constexpr int nv = NV;
   const long long base = (long long)row * cols;
   const K3mDrop din = k3m_drop_init(seed, p_in), dout = k3m_drop_init(seed, p_out);
   float v[MAXV8][8];
-#pragma unroll
-  for (int j = 0; j < MAXV8; ++j)
-    if (j < nv) ld8bf(x + base + (l + 32 * j) * 8, v[j]);
   float rv[MAXV8][8];
-  if (res) {
+  const bf16_t* rp = res ? res : x;   // unconditional loads, all issued before the arithmetic
 #pragma unroll
-    for (int j = 0; j < MAXV8; ++j)
-      if (j < nv) ld8bf(res + base + (l + 32 * j) * 8, rv[j]);
-  }
+  for (int j = 0; j < nv; ++j) ld8bf(x + base + (l + 32 * j) * 8, v[j]);
+#pragma unroll
+  for (int j = 0; j < nv; ++j) ld8bf(rp + base + (l + 32 * j) * 8, rv[j]);
   float sum = 0.f;
 #pragma unroll
   for (int j = 0; j < MAXV8; ++j)
@@ -377,6 +393,7 @@ __global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const bf16_t* __restri
     }
 }
 
+template <int NV>
 __global__ __launch_bounds__(256) void ln_bwd_bf16_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ xhat,
                                                           const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                           bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
@@ -384,8 +401,8 @@ __global__ __launch_bounds__(256) void ln_bwd_bf16_kernel(const bf16_t* __restri
                                                           float p_out, uint64_t seed, uint64_t off_in, uint64_t off_out,
                                                           int acc_res, int want_sum) {
   __shared__ float red[4][1024];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, l = lane & 31;
-  const int nv = cols >> 8;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, l = lane & 31;
+  constexpr int nv = NV;
   const K3mDrop din = k3m_drop_init(seed, p_in), dout = k3m_drop_init(seed, p_out);
   float pg[MAXV8][8], pb[MAXV8][8], px[MAXV8][8];
 #pragma unroll
@@ -397,13 +414,14 @@ __global__ __launch_bounds__(256) void ln_bwd_bf16_kernel(const bf16_t* __restri
   const int S = gridDim.x * 8;
   for (int row = blockIdx.x * 8 + (threadIdx.x >> 5); row < rows; row += S) {
     const long long base = (long long)row * cols;
-    float d[MAXV8][8], xv[MAXV8][8];
+    float d[MAXV8][8], xv[MAXV8][8], old[MAXV8][8];
+    const bf16_t* rsrc = acc_res ? dres : dy;   // every load of the row issued before the arithmetic
 #pragma unroll
-    for (int j = 0; j < MAXV8; ++j)
-      if (j < nv) {
-        ld8bf(dy + base + (l + 32 * j) * 8, d[j]);
-        ld8bf(xhat + base + (l + 32 * j) * 8, xv[j]);
-      }
+    for (int j = 0; j < nv; ++j) {
+      ld8bf(dy + base + (l + 32 * j) * 8, d[j]);
+      ld8bf(xhat + base + (l + 32 * j) * 8, xv[j]);
+      ld8bf(rsrc + base + (l + 32 * j) * 8, old[j]);
+    }
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < MAXV8; ++j)
@@ -434,10 +452,8 @@ __global__ __launch_bounds__(256) void ln_bwd_bf16_kernel(const bf16_t* __restri
 #pragma unroll
         for (int e = 0; e < 8; ++e) ds[e] = (d[j][e] * g[e] - m1 - xv[j][e] * m2) * rs;
         if (acc_res) {
-          float old[8];
-          ld8bf(dres + base + c, old);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) dr[e] = ds[e] + old[e];
+          for (int e = 0; e < 8; ++e) dr[e] = ds[e] + old[j][e];
         } else {
 #pragma unroll
           for (int e = 0; e < 8; ++e) dr[e] = ds[e];
@@ -709,14 +725,28 @@ extern "C" int k3m_ln_fwd(const void* x, const void* res, const float* gamma, co
                           uint64_t off_in, uint64_t off_out, int dtype, hipStream_t st) {
   K3M_ARG(x && gamma && beta && y && rows >= 0 && cols % 256 == 0 && cols <= 1024 && cols > 0);
   if (rows == 0) return 0;
+  const int nv = cols >> 8;
+#define K3M_LN_NV(F)   \
+  switch (nv) {        \
+    case 1: F(1); break; \
+    case 2: F(2); break; \
+    case 3: F(3); break; \
+    default: F(4);       \
+  }
   if (dtype == K3M_BF16 && kLnBf16Vec && rows >= LN_VEC_FWD_ROWS) {
-    hipLaunchKernelGGL(ln_fwd_bf16_kernel, dim3(k3m_cdiv(rows, 8)), dim3(256), 0, st, (const bf16_t*)x,
-                       (const bf16_t*)res, gamma, beta, (bf16_t*)y, (bf16_t*)xhat, rstd, rows, cols, eps, p_in, p_out,
-                       seed, off_in, off_out);
+#define K3M_LNF16(NV_)                                                                                        \
+  hipLaunchKernelGGL(ln_fwd_bf16_kernel<NV_>, dim3(k3m_cdiv(rows, 8)), dim3(256), 0, st, (const bf16_t*)x,   \
+                      (const bf16_t*)res, gamma, beta, (bf16_t*)y, (bf16_t*)xhat, rstd, rows, cols, eps, p_in, \
+                      p_out, seed, off_in, off_out)
+    K3M_LN_NV(K3M_LNF16);
+#undef K3M_LNF16
   } else {
-    DISPATCH_T(dtype, hipLaunchKernelGGL(ln_fwd_kernel<T>, dim3(k3m_cdiv(rows, 4)), dim3(256), 0, st,
-                                         (const T*)x, (const T*)res, gamma, beta, (T*)y, (T*)xhat, rstd, rows, cols, eps,
-                                         p_in, p_out, seed, off_in, off_out));
+#define K3M_LNF(NV_)                                                                                          \
+  hipLaunchKernelGGL((ln_fwd_kernel<T, NV_>), dim3(k3m_cdiv(rows, 4)), dim3(256), 0, st, (const T*)x,       \
+                      (const T*)res, gamma, beta, (T*)y, (T*)xhat, rstd, rows, cols, eps, p_in, p_out, seed,  \
+                      off_in, off_out)
+    DISPATCH_T(dtype, K3M_LN_NV(K3M_LNF));
+#undef K3M_LNF
   }
   K3M_CHECK_LAUNCH();
   return 0;
@@ -743,14 +773,21 @@ extern "C" int k3m_ln_bwd_slabs(const void* dy, const void* xhat, const float* r
   K3M_ARG(cols % 256 == 0 && cols <= 1024 && rows >= 0);
   if (rows == 0) return 0;
   const int nb = ln_bwd_slab_count(rows);
+  const int nv = cols >> 8;
   if (dtype == K3M_BF16 && kLnBf16Vec && rows >= LN_VEC_BWD_ROWS) {
-    hipLaunchKernelGGL(ln_bwd_bf16_kernel, dim3(nb), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)xhat, rstd,
-                       gamma, (bf16_t*)dres, (bf16_t*)dx, ws, rows, cols, p_in, p_out, seed, off_in, off_out, acc_res,
-                       want_sum);
+#define K3M_LNB16(NV_)                                                                                         \
+  hipLaunchKernelGGL(ln_bwd_bf16_kernel<NV_>, dim3(nb), dim3(256), 0, st, (const bf16_t*)dy,                  \
+                      (const bf16_t*)xhat, rstd, gamma, (bf16_t*)dres, (bf16_t*)dx, ws, rows, cols, p_in, p_out, \
+                      seed, off_in, off_out, acc_res, want_sum)
+    K3M_LN_NV(K3M_LNB16);
+#undef K3M_LNB16
   } else {
-    DISPATCH_T(dtype, hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3(nb), dim3(256), 0, st, (const T*)dy, (const T*)xhat,
-                                         rstd, gamma, (T*)dres, (T*)dx, ws, rows, cols, p_in, p_out, seed, off_in,
-                                         off_out, acc_res, want_sum));
+#define K3M_LNB(NV_)                                                                                           \
+  hipLaunchKernelGGL((ln_bwd_kernel<T, NV_>), dim3(nb), dim3(256), 0, st, (const T*)dy, (const T*)xhat, rstd, \
+                      gamma, (T*)dres, (T*)dx, ws, rows, cols, p_in, p_out, seed, off_in, off_out, acc_res,    \
+                      want_sum)
+    DISPATCH_T(dtype, K3M_LN_NV(K3M_LNB));
+#undef K3M_LNB
   }
   K3M_CHECK_LAUNCH();
   return 0;

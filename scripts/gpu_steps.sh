@@ -67,6 +67,8 @@ for s in "$@"; do
     abkm) step abkm 900 scripts/ab_env.sh K3M_FLASH_BWD_KM "0 1" 3 --config 3 --steps 10 --warmup 4 ;;
     b16lab) for r in 1 2; do for lab in 0 1 2 3; do
               K3M_B16_LAB=$lab step b16lab_${lab}_$r 300 python scripts/gemm_bench.py all 20 bf16; done; done ;;
+    tmode) step tmode 600 python -u -m pytest tests/test_gpu_train_mode_parity.py -v --timeout 300 --timeout-method thread ;;
+    prof32) export TMPDIR=/tmp; step prof32 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof32 -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
