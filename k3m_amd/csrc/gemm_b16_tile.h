@@ -731,4 +731,247 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_persist_kernel(GemmGroup
   }
 }
 
+
+// ====================================================================== two workgroups per CU
+// The 256x256 walk above runs ONE 8-wave workgroup per CU (128 KB of LDS stages): while it runs its
+// epilogue (the bias / GELU / dGELU VALU and the C stores: a third of a K = 768 GEMM) no MFMA issues on
+// that CU, and the lab timings (profiles/r4a_ab_flash_km_and_b16_lab.txt: stores off -13 %, epilogue
+// math ~ -25 % on FFN1) put most of the K = 768 GEMMs' loss there.  The dual form fits TWO workgroups
+// on a CU so one's epilogue overlaps the other's main loop (MFMA and VALU are separate pipes; vmcnt is
+// per wave, so one workgroup's stores never hold the other's DMA waits):
+//  * tile 256 x 128 x 32, 4 waves (2 x 2, each 128 x 64 — the same per-wave tile and accumulators);
+//  * THREE LDS stages of 24 KB (72 KB per workgroup, 144 KB for the pair); operands by LDS-DMA with the
+//    DMA of k-tile t+4 issued at iteration t into the stage just read, two k-tiles in flight across each
+//    barrier (counted vmcnt), fragment reads of tile t+1 under the MFMAs of tile t;
+//  * K-contiguous images [TILE][32] (64-B rows): chunk c of row r at slot c ^ g((r >> 2) & 3) with
+//    g = {0, 2, 3, 1}, conflict-free for the ds_read_b128 lane groups of both MFMA shapes;
+//    MN-contiguous images [32][TILE] as above (mn_off), transposing reads;
+//  * persistent walk over 2 x CUs workgroups; epilogue through LDS exactly as the 8-wave kernel (same
+//    arithmetic per element: bit-identical C).
+constexpr int BKD = 32;
+
+__device__ __forceinline__ int swz4(int r) { return (0x1320 >> (((r >> 2) & 3) << 2)) & 3; }
+__device__ __forceinline__ int kc4_off(int r, int c) { return r * BKD + ((c ^ swz4(r)) << 3); }
+
+template <bool KC, int TILE, int NT>
+struct LoaderD {
+  static constexpr int INSTS = TILE * BKD * 2 / 1024;   // wave instructions per k-tile
+  static constexpr int NW = NT / 64;
+  static constexpr int NI = INSTS / NW;                  // per wave
+  static_assert(INSTS % NW == 0, "tile must split evenly over the waves");
+  const uint16_t* base;
+  long long step;
+  uint32_t off[NI];
+  int lds0;
+  __device__ __forceinline__ void init(const uint16_t* __restrict__ a, long long ld, int mn0, int kbeg, int MN) {
+    const int l = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    lds0 = w * 512;
+    base = a + (KC ? (long long)kbeg : (long long)kbeg * ld);
+    step = KC ? BKD : BKD * ld;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int inst = w + NW * i;
+      if constexpr (KC) {   // 16 rows x 4 chunks per instruction
+        const int row = inst * 16 + (l >> 2), slot = l & 3;
+        const int ch = slot ^ swz4(row);
+        off[i] = (uint32_t)((long long)min(mn0 + row, MN - 1) * ld + ch * 8);
+      } else {
+        constexpr int CPR = TILE / 8, RPI = 64 / CPR;
+        const int kr = inst * RPI + l / CPR, slot = l % CPR;
+        const int ch = slot ^ (((kr & 3) << 2) | ((kr >> 2) & 3));
+        off[i] = (uint32_t)((long long)kr * ld + max(0, min(mn0 + ch * 8, MN - 8)));
+      }
+    }
+  }
+  __device__ __forceinline__ void issue(uint16_t* img) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) glds16(base + off[i], img + lds0 + i * NW * 512);
+    base += step;
+  }
+};
+
+// s_waitcnt vmcnt(N) only (expcnt, lgkmcnt at their maxima: not waited for)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// Fragments of a wave's 128 x 64 slab: 16x16x32 — one set is a whole 32-deep k-tile (8 A x 4 B);
+// 32x32x16 — one set is one 16-deep substep (4 A x 2 B), two per k-tile (the transposing reads of
+// MN-contiguous operands take two ds_read_b64_tr_b16 per fragment: whole-tile sets spilled)
+template <int MF, bool AK, bool BK_, int TBM, int TBN>
+struct FragsD;
+template <bool AK, bool BK_, int TBM, int TBN>
+struct FragsD<16, AK, BK_, TBM, TBN> {
+  bf16x8 a[8], b[4];
+  __device__ __forceinline__ void read(const uint16_t* st, int, int wm, int wn, int lane) {
+    const uint16_t* sb = st + TBM * BKD;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if constexpr (AK) a[i] = *reinterpret_cast<const bf16x8*>(st + kc4_off(wm + 16 * i + (lane & 15), lane >> 4));
+      else a[i] = frag<false, TBM>(st, wm + 16 * i, 0, lane);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (BK_) b[j] = *reinterpret_cast<const bf16x8*>(sb + kc4_off(wn + 16 * j + (lane & 15), lane >> 4));
+      else b[j] = frag<false, TBN>(sb, wn + 16 * j, 0, lane);
+    }
+  }
+  template <typename AccT>
+  __device__ __forceinline__ void mfma(AccT& acc) const {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc.v[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc.v[i][j], 0, 0, 0);
+  }
+};
+template <bool AK, bool BK_, int TBM, int TBN>
+struct FragsD<32, AK, BK_, TBM, TBN> {
+  bf16x8 a[4], b[2];
+  __device__ __forceinline__ void read(const uint16_t* st, int s, int wm, int wn, int lane) {
+    const uint16_t* sb = st + TBM * BKD;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (AK) a[i] = *reinterpret_cast<const bf16x8*>(st + kc4_off(wm + 32 * i + (lane & 31), 2 * s + (lane >> 5)));
+      else a[i] = frag32<false, TBM>(st, wm + 32 * i, s, lane);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if constexpr (BK_) b[j] = *reinterpret_cast<const bf16x8*>(sb + kc4_off(wn + 32 * j + (lane & 31), 2 * s + (lane >> 5)));
+      else b[j] = frag32<false, TBN>(sb, wn + 32 * j, s, lane);
+    }
+  }
+  template <typename AccT>
+  __device__ __forceinline__ void mfma(AccT& acc) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc.v[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc.v[i][j], 0, 0, 0);
+  }
+};
+
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int MF>
+__device__ __forceinline__ void mainloop_d(const uint16_t* __restrict__ A, long long lda,
+                                           const uint16_t* __restrict__ B, long long ldb, int M, int N, int m0,
+                                           int n0, int kbeg, int kend, uint16_t* smem,
+                                           Acc<MF, TBM / WM, TBN / WN>& acc) {
+  constexpr int NT = 64 * WM * WN, STAGE = (TBM + TBN) * BKD;
+  static_assert(TBM / WM == 128 && TBN / WN == 64, "per-wave slab 128 x 64");
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = (w / WN) * (TBM / WM), wn = (w % WN) * (TBN / WN);
+  if constexpr (MF == 16) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc.v[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc.v[i][j][r] = 0.f;
+  }
+  LoaderD<AK, TBM, NT> la;
+  LoaderD<BK_, TBN, NT> lb;
+  la.init(A, lda, m0, kbeg, M);
+  lb.init(B, ldb, n0, kbeg, N);
+  constexpr int NI = LoaderD<AK, TBM, NT>::NI + LoaderD<BK_, TBN, NT>::NI;   // DMA instructions per k-tile
+  const int nk = kend > kbeg ? (kend - kbeg) / BKD : 0;
+  if (nk == 0) return;
+  auto issue = [&](int stg) {
+    la.issue(smem + stg * STAGE);
+    lb.issue(smem + stg * STAGE + TBM * BKD);
+  };
+  issue(0);
+  if (nk > 1) issue(1);
+  if (nk > 2) issue(2);
+  if (nk > 2) wait_vm<2 * NI>();
+  else if (nk > 1) wait_vm<NI>();
+  else wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  FragsD<MF, AK, BK_, TBM, TBN> F, G;
+  F.read(smem, 0, wm, wn, lane);
+  if constexpr (MF == 16) {
+    // iteration t: tile t+1 -> the other set under the MFMAs of tile t; wait for tile t+2 (tile t+3 may stay
+    // in flight), barrier, DMA tile t+4 into the stage just read
+    if (nk > 2) wait_vm<NI>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (nk > 3) issue(0);   // tile 3 -> the stage of tile 0 (already in F)
+    int rs = 1;              // stage of tile t+1
+    auto step = [&](FragsD<MF, AK, BK_, TBM, TBN>& cur, FragsD<MF, AK, BK_, TBM, TBN>& nxt, int t) {
+      nxt.read(smem + rs * STAGE, 0, wm, wn, lane);   // past the last tile: a stale stage nobody uses
+      __builtin_amdgcn_sched_barrier(0);
+      cur.mfma(acc);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (t + 3 < nk) wait_vm<NI>();
+      else wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 4 < nk) issue(rs);
+      rs = rs == 2 ? 0 : rs + 1;
+    };
+    int t = 0;
+    for (; t + 1 < nk; t += 2) {
+      step(F, G, t);
+      step(G, F, t + 1);
+    }
+    if (t < nk) step(F, G, t);
+  } else {
+    // iteration t: substep 1 of tile t -> G under the MFMAs of substep 0 (F); wait for tile t+1 (tile t+2 may
+    // stay in flight), barrier, DMA tile t+3 into tile t's stage (both substeps read), substep 0 of tile
+    // t+1 -> F under the MFMAs of G
+    int cs = 0;   // stage of tile t
+    for (int t = 0; t < nk; ++t) {
+      const int ns = cs == 2 ? 0 : cs + 1;
+      G.read(smem + cs * STAGE, 1, wm, wn, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      F.mfma(acc);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (t + 2 < nk) wait_vm<NI>();
+      else wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 3 < nk) issue(cs);
+      F.read(smem + ns * STAGE, 0, wm, wn, lane);   // past the last tile: a stale stage nobody uses
+      __builtin_amdgcn_sched_barrier(0);
+      G.mfma(acc);
+      __builtin_amdgcn_sched_barrier(0);
+      cs = ns;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();   // the epilogue reuses the stages
+}
+
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF>
+__global__ __launch_bounds__(64 * WM * WN, 2) void gemm_dual_kernel(GemmGroup grp) {
+  constexpr int WORDS = 3 * (TBM + TBN) * BKD;
+  static_assert(EpiLds<TBM, TBN, WM, WN>::E <= WORDS, "epilogue staging exceeds the LDS stages");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[WORDS];
+  const int total = grp.start[grp.count];
+  int u = blockIdx.x;
+  if (u >= total) return;
+  for (;;) {   // uniform over the workgroup: every wave leaves together
+    PUnit<TBM, TBN, WM, WN> cur;
+    cur.decode(grp, u);
+    const K3mGemm& g = grp.g[cur.p];
+    Acc<MF, TBM / WM, TBN / WN> acc;
+    mainloop_d<TBM, TBN, WM, WN, AK, BK_, MF>(static_cast<const uint16_t*>(g.a), g.lda,
+                                              static_cast<const uint16_t*>(g.b), g.ldb, g.m, g.n, cur.m0, cur.n0,
+                                              cur.kbeg, cur.kend, smem, acc);
+    epilogue<TBM, TBN, WM, WN, EPI, CT>(g, cur.m0, cur.n0, smem, acc, cur.slice);
+    u += gridDim.x;
+    if (u >= total) break;
+  }
+}
+
 }  // namespace k3m_b16

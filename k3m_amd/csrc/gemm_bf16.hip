@@ -454,8 +454,8 @@ long long nb_of(const K3mGemm& g, int bm, int bn) {
 // MFMA shape per operand layout: 16x16x32 when B is K-contiguous (forward), 32x32x16 when it is
 // MN-contiguous (input and weight gradients: their transposing fragment reads fit the LDS counter
 // per 16-deep substep); K3M_B16_MF=16 / 32 forces one shape everywhere (A/B).
-const int kMF = k3m_env_int("K3M_B16_MF", 0);
-inline bool use_mf32(bool bk) { return kMF == 32 || (kMF != 16 && !bk); }
+// (the round-3 K3M_B16_MF override is gone: one MFMA shape per operand layout halves the instantiations)
+template <bool BK_> constexpr int mf_of() { return BK_ ? 16 : 32; }
 
 // The large-tile GEMMs as a persistent walk of min(units, CUs) workgroups (gemm_persist_kernel): bit-identical,
 // bf16 step +0.4 % in three interleaved pairs (profiles/r3_ab_b16_persist.txt); K3M_B16_PERSIST=0 launches one
@@ -480,8 +480,32 @@ const bool kB16Prefetch = k3m_env_flag("K3M_B16_PREFETCH", false);
 const int kB16Lab = k3m_env_int("K3M_B16_LAB", 0);
 const int kB16Stagger = k3m_env_int("K3M_B16_STAGGER", 500);
 
+// K3M_B16_DUAL=1: the large-tile GEMMs on the two-workgroups-per-CU kernel (gemm_dual_kernel: 256 x 128 x 32
+// tiles, 4 waves, three LDS stages) instead of the one-workgroup 256 x 256 / 256 x 128 walk
+const bool kB16Dual = k3m_env_flag("K3M_B16_DUAL", false);
+
+long long nb_of(const K3mGemm& g, int bm, int bn);
+
+template <bool AK, bool BK_, int EPI, typename CT, int MF>
+void dual_launch(const k3m_b16::GemmGroup& grp_in, hipStream_t st) {
+  k3m_b16::GemmGroup grp = grp_in;   // units re-counted for the 256 x 128 tiles
+  int nb = 0;
+  for (int i = 0; i < grp.count; ++i) {
+    grp.start[i] = nb;
+    nb += (int)nb_of(grp.g[i], 256, 128);
+  }
+  grp.start[grp.count] = nb;
+  const int nblk = nb < 2 * b16_cus() ? nb : 2 * b16_cus();
+  hipLaunchKernelGGL((k3m_b16::gemm_dual_kernel<256, 128, 2, 2, AK, BK_, EPI, CT, MF>), dim3(nblk), dim3(256), 0, st,
+                     grp);
+}
+
 template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF>
 void persist_launch(const k3m_b16::GemmGroup& grp_in, hipStream_t st) {
+  if (kB16Dual) {
+    dual_launch<AK, BK_, EPI, CT, MF>(grp_in, st);
+    return;
+  }
   k3m_b16::GemmGroup grp = grp_in;
   grp.lab = kB16Lab;
   grp.stagger = kB16Stagger;
@@ -530,8 +554,7 @@ int big_launch_epi_mf(const K3mGemm& g, hipStream_t st) {
 
 template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, typename CT>
 int big_launch_epi(const K3mGemm& g, hipStream_t st) {
-  return use_mf32(BK_) ? big_launch_epi_mf<TBM, TBN, WM, WN, AK, BK_, CT, 32>(g, st)
-                       : big_launch_epi_mf<TBM, TBN, WM, WN, AK, BK_, CT, 16>(g, st);
+  return big_launch_epi_mf<TBM, TBN, WM, WN, AK, BK_, CT, mf_of<BK_>()>(g, st);
 }
 
 template <int TBM, int TBN, int WM, int WN>
@@ -579,8 +602,7 @@ int big_grouped_epi_mf(const k3m_b16::GemmGroup& grp, int epi, hipStream_t st) {
 
 template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, typename CT>
 int big_grouped_epi(const k3m_b16::GemmGroup& grp, int epi, hipStream_t st) {
-  return use_mf32(BK_) ? big_grouped_epi_mf<TBM, TBN, WM, WN, AK, BK_, CT, 32>(grp, epi, st)
-                       : big_grouped_epi_mf<TBM, TBN, WM, WN, AK, BK_, CT, 16>(grp, epi, st);
+  return big_grouped_epi_mf<TBM, TBN, WM, WN, AK, BK_, CT, mf_of<BK_>()>(grp, epi, st);
 }
 
 template <int TBM, int TBN, int WM, int WN>

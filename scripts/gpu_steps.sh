@@ -69,6 +69,10 @@ for s in "$@"; do
               K3M_B16_LAB=$lab step b16lab_${lab}_$r 300 python scripts/gemm_bench.py all 20 bf16; done; done ;;
     tmode) step tmode 600 python -u -m pytest tests/test_gpu_train_mode_parity.py -v --timeout 300 --timeout-method thread ;;
     prof32) export TMPDIR=/tmp; step prof32 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof32 -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    dual) step dualbit 400 python -u -m pytest tests/test_gpu_gemm_b16_dual.py -v --timeout 300 --timeout-method thread
+          K3M_B16_DUAL=1 step dualbig 600 python -u -m pytest tests/test_gpu_gemm_b16_big.py tests/test_gpu_gemm_bf16.py -q --timeout 300 --timeout-method thread
+          for d in 0 1; do K3M_B16_DUAL=$d step dualgemm_$d 300 python scripts/gemm_bench.py all 20 bf16; done
+          step abdual 900 scripts/ab_env.sh K3M_B16_DUAL "0 1" 3 --config 3 --steps 10 --warmup 4 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
