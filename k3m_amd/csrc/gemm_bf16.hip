@@ -480,9 +480,13 @@ const bool kB16Prefetch = k3m_env_flag("K3M_B16_PREFETCH", false);
 const int kB16Lab = k3m_env_int("K3M_B16_LAB", 0);
 const int kB16Stagger = k3m_env_int("K3M_B16_STAGGER", 500);
 
-// K3M_B16_DUAL=1: the large-tile GEMMs on the two-workgroups-per-CU kernel (gemm_dual_kernel: 256 x 128 x 32
-// tiles, 4 waves, three LDS stages) instead of the one-workgroup 256 x 256 / 256 x 128 walk
-const bool kB16Dual = k3m_env_flag("K3M_B16_DUAL", false);
+// K3M_B16_DUAL: the large-tile GEMMs on the two-workgroups-per-CU kernel (gemm_dual_kernel: 256 x 128 x 32
+// tiles, 4 waves, three LDS stages) instead of the one-workgroup 256 x 256 / 256 x 128 walk.  0 = never,
+// 1 = always, 2 (default) = the GELU / dGELU epilogues only: there one workgroup's epilogue VALU overlaps the
+// other's MFMAs (FFN1 fwd -2 %, FFN2 dgrad+dGELU -4 %, co-attention PV FFN1 -14 %), while the plain main loop
+// is 10-25 % slower at 256 x 128 x 32 (1.5x the operand bytes per MFMA of 256 x 256; profiles/r4b_ab_dual.txt)
+const int kB16Dual = k3m_env_int("K3M_B16_DUAL", 2);
+constexpr bool dual_epi(int epi) { return epi == K3M_EPI_BIAS_GELU || epi == K3M_EPI_DGELU; }
 
 long long nb_of(const K3mGemm& g, int bm, int bn);
 
@@ -502,7 +506,7 @@ void dual_launch(const k3m_b16::GemmGroup& grp_in, hipStream_t st) {
 
 template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF>
 void persist_launch(const k3m_b16::GemmGroup& grp_in, hipStream_t st) {
-  if (kB16Dual) {
+  if (kB16Dual == 1 || (kB16Dual == 2 && dual_epi(EPI))) {
     dual_launch<AK, BK_, EPI, CT, MF>(grp_in, st);
     return;
   }

@@ -73,6 +73,10 @@ for s in "$@"; do
           K3M_B16_DUAL=1 step dualbig 600 python -u -m pytest tests/test_gpu_gemm_b16_big.py tests/test_gpu_gemm_bf16.py -q --timeout 300 --timeout-method thread
           for d in 0 1; do K3M_B16_DUAL=$d step dualgemm_$d 300 python scripts/gemm_bench.py all 20 bf16; done
           step abdual 900 scripts/ab_env.sh K3M_B16_DUAL "0 1" 3 --config 3 --steps 10 --warmup 4 ;;
+    dualbit) step dualbit 400 python -u -m pytest tests/test_gpu_gemm_b16_dual.py -v --timeout 300 --timeout-method thread ;;
+    abdual2) step abdual2 900 scripts/ab_env.sh K3M_B16_DUAL "0 2" 3 --config 3 --steps 10 --warmup 4 ;;
+    attnbf) step attnbf 300 python scripts/attn_bench.py bf16 ;;
+    attn32) step attn32 300 python scripts/attn_bench.py fp32 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
