@@ -25,6 +25,7 @@ Mirrors the driver loop of train_concap_struc.py:466-589.
 """
 import collections
 import math
+import os
 
 import torch
 
@@ -113,6 +114,39 @@ def optimizer_runs(fp, weight_decay=0.01, lr_mult=None, frozen_names=()):
     return [(a, (b - a + 3) // 4 * 4, wd, mu) for a, b, wd, mu in runs]
 
 
+def block_runs(fp, weight_decay=0.01, lr_mult=None, frozen_names=()):
+    """optimizer_runs() cut at the gradient-readiness blocks of the wide engine (k3m_amd.ddp._block_of:
+    heads / fusion / structure, each encoder block, the embeddings): {block: [(offset, length, wd, lr_mult)]},
+    so that a block's AdamW can run as soon as the backward has finished that block."""
+    from .ddp import _block_of
+    lr_mult = lr_mult or {}
+    frozen_names = set(frozen_names)
+    per = {}
+    for name, shape in fp.spec:
+        if segment_of(name) == "frozen" or name in frozen_names:
+            continue
+        o = fp.offsets[name]
+        per.setdefault(_block_of(name), []).append(
+            (o, o + math.prod(shape), weight_decay if segment_of(name) == "decay" else 0.0, float(lr_mult.get(name, 1.0))))
+    out = {}
+    for blk, items in per.items():
+        items.sort()
+        runs = []
+        for a, b, wd, mu in items:
+            if runs and runs[-1][2] == wd and runs[-1][3] == mu and a - runs[-1][1] < 4:
+                runs[-1][1] = b
+            else:
+                runs.append([a, b, wd, mu])
+        out[blk] = [(a, (b - a + 3) // 4 * 4, wd, mu) for a, b, wd, mu in runs]
+    return out
+
+
+# AdamW of each gradient block on a side stream as soon as the backward has finished that block (single
+# process, no gradient accumulation pending): the HBM-bound sweep overlaps the rest of the backward instead of
+# following it.  K3M_OPT_OVERLAP=0 restores the one sweep after the backward.
+OPT_OVERLAP = os.environ.get("K3M_OPT_OVERLAP", "1") != "0"
+
+
 class LossWatch(object):
     """Asynchronous NaN / inf fail-fast: the loss of each step is copied into pinned host memory
     behind an event; the copy is inspected once the event has completed (a later step), so the
@@ -146,6 +180,10 @@ class LossWatch(object):
 
     def flush(self):
         self.poll(force=True)
+
+
+def fp_is_cuda(eng):
+    return eng.fp.data.is_cuda
 
 
 class Trainer(object):
@@ -191,6 +229,9 @@ class Trainer(object):
         self.v = torch.zeros(nopt, dtype=torch.float32, device=fp.device)
         self.watch = LossWatch() if nan_check else None
         self.dropout = True   # False: the step runs without dropout (model.eval() forward; parity runs)
+        self.block_runs = block_runs(fp, weight_decay, lr_mult, frozen_names)
+        self.opt_stream = None
+        self.overlap = OPT_OVERLAP
 
     def evaluate(self, batch, noise=None, ent_neg=None, val_neg=None):
         """The validation forward of train_concap_struc.py:612-688 (model.eval(), no gradients): returns
@@ -218,6 +259,50 @@ class Trainer(object):
         return mult * self.current_lr()
 
     # ---------------------------------------------------------------- optimizer
+    def _adam_runs(self, runs, step, grad_scale, flags):
+        fp = self.engine.fp
+        for off, n, wd, mult in runs:
+            if n == 0:
+                continue
+            sh = fp.data16[off:].data_ptr() if fp.data16 is not None else None
+            L.call("k3m_adamw_ex", fp.data[off:].data_ptr(), fp.grad[off:].data_ptr(), self.m[off:].data_ptr(),
+                   self.v[off:].data_ptr(), sh, n, self.run_lr(off, mult), self.beta1, self.beta2, self.eps, wd, step,
+                   grad_scale, flags, L.stream())
+
+    def _overlap_begin(self):
+        """State of an overlapped optimizer step: blocks still to update and the side stream."""
+        dev = self.engine.fp.device
+        if self.opt_stream is None:
+            self.opt_stream = torch.cuda.Stream(device=dev)
+        self._pending = set(self.block_runs)
+        self._flags = L.ADAM_ZERO_GRAD | (L.ADAM_APEX if self.optimizer == "fused_adam" else 0)
+
+    def _overlap_block(self, blk):
+        if blk not in self._pending:
+            return
+        self._pending.discard(blk)
+        ev = torch.cuda.Event()
+        ev.record()
+        with torch.cuda.stream(self.opt_stream):
+            self.opt_stream.wait_event(ev)
+            self._adam_runs(self.block_runs[blk], self.global_step + 1, 1.0, self._flags)
+
+    def _overlap_hook(self, kind, index):
+        # the heads / fusion / structure gradients are final before the first encoder block's (ddp.grad_ready)
+        self._overlap_block(("head", 0))
+        self._overlap_block((kind, index))
+
+    def _overlap_finish(self):
+        fp = self.engine.fp
+        fresh = fp.shadow_fresh
+        for blk in sorted(self._pending):
+            self._overlap_block(blk)
+        torch.cuda.current_stream(fp.device).wait_stream(self.opt_stream)
+        for name in self.excluded:   # --freeze: gradients the optimizer skips are dropped as well
+            fp.g[name].zero_()
+        fp.shadow_fresh = fresh
+        self.global_step += 1
+
     def optimizer_step(self, grad_scale=1.0, zero_grad=True):
         """One optimizer step over every run; the gradient buffer is zeroed in the same sweep."""
         fp = self.engine.fp
@@ -277,20 +362,29 @@ class Trainer(object):
             out["masked_img_loss"] * self.loss_img_weight
         last = self.micro + 1 == self.accum_steps
         sync = self.ddp is not None and last
+        overlap = (self.overlap and last and self.ddp is None and self.ADAMW is None and fp_is_cuda(eng))
+        hook = None
         if sync:
             self.ddp.begin(eng)
-        eng.backward(ctx, w_mlm=w, w_img=self.loss_img_weight * w, w_lpm=w,
-                     grad_ready=self.ddp.grad_ready if sync else None)
+            hook = self.ddp.grad_ready
+        elif overlap:
+            eng.check_hints()   # a completed label-count check that failed raises before any update
+            self._overlap_begin()
+            hook = self._overlap_hook
+        eng.backward(ctx, w_mlm=w, w_img=self.loss_img_weight * w, w_lpm=w, grad_ready=hook)
         if self.watch is not None:
             self.watch.push(self.global_step, out["loss"])
         self.micro += 1
         if last:
-            eng.check_hints()   # a completed label-count check that failed raises before the update
-            scale = 1.0
-            if sync:
-                self.ddp.finish()
-                scale = 1.0 / self.ddp.world
-            self.optimizer_step(grad_scale=scale)
+            if overlap:
+                self._overlap_finish()
+            else:
+                eng.check_hints()   # a completed label-count check that failed raises before the update
+                scale = 1.0
+                if sync:
+                    self.ddp.finish()
+                    scale = 1.0 / self.ddp.world
+                self.optimizer_step(grad_scale=scale)
             self.micro = 0
             eng.step_count += 1
         return out

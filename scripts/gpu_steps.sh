@@ -77,6 +77,8 @@ for s in "$@"; do
     abdual2) step abdual2 900 scripts/ab_env.sh K3M_B16_DUAL "0 2" 3 --config 3 --steps 10 --warmup 4 ;;
     attnbf) step attnbf 300 python scripts/attn_bench.py bf16 ;;
     attn32) step attn32 300 python scripts/attn_bench.py fp32 ;;
+    abopt) step abopt3 900 scripts/ab_env.sh K3M_OPT_OVERLAP "0 1" 3 --config 3 --steps 10 --warmup 4
+           step abopt2 900 scripts/ab_env.sh K3M_OPT_OVERLAP "0 1" 2 --config 2 --steps 8 --warmup 4 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
