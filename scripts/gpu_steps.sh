@@ -79,6 +79,7 @@ for s in "$@"; do
     attn32) step attn32 300 python scripts/attn_bench.py fp32 ;;
     abopt) step abopt3 900 scripts/ab_env.sh K3M_OPT_OVERLAP "0 1" 3 --config 3 --steps 10 --warmup 4
            step abopt2 900 scripts/ab_env.sh K3M_OPT_OVERLAP "0 1" 2 --config 2 --steps 8 --warmup 4 ;;
+    logiterr) step logiterr 400 python scripts/bf16_logit_errors.py gpurun_out/r4_bf16_logit_errors.json ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
