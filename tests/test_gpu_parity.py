@@ -107,8 +107,16 @@ BF16_LOSS_RTOL = 1e-2
 BF16_GRAD_COS = 0.98
 BF16_GRAD_NORM_RTOL = 3e-2
 BF16_GLOBAL_COS = 0.995
-BF16_LOGIT_RTOL = 0.35   # a few elements of rows with small logits reach ~0.22 (cfg5)
+# bf16 logit bars, set from the measured error distribution over the five goldens
+# (profiles/r4_bf16_logit_errors.json, scripts/bf16_logit_errors.py; error = |bf16 - ref| / row max |ref|):
+# worst element 0.218 (cfg5), worst 99th percentile 0.063 (cfg4), worst per-column mean 0.0147 (region head,
+# bs2_hard), worst mean 0.0067, worst logsumexp error 1.0e-3 absolute.  A systematic error in a few vocabulary
+# or region columns shows in the per-column mean, not in the max or the global mean.
+BF16_LOGIT_RTOL = 0.25
 BF16_LOGIT_MEAN = 1e-2
+BF16_LOGIT_P99 = 0.08
+BF16_LOGIT_COLMEAN = 0.02
+BF16_LSE_ATOL = 5e-3
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -128,8 +136,9 @@ def test_bf16_engine_close_to_reference_golden(dev, case):
     torch.cuda.synchronize()
     # bf16 encoder: every logit within BF16_LOGIT_RTOL of its row's max |logit|, mean error BF16_LOGIT_MEAN
     check_logits(g, out["mlm_logits"].cpu().numpy(), g["logit/img_rows"], BF16_LOGIT_RTOL, case + " bf16",
-                 mean_rtol=BF16_LOGIT_MEAN)
-    check_img_logits(g, out["img_logits"].cpu().numpy(), BF16_LOGIT_RTOL, case + " bf16", mean_rtol=BF16_LOGIT_MEAN)
+                 mean_rtol=BF16_LOGIT_MEAN, p99=BF16_LOGIT_P99, col_mean=BF16_LOGIT_COLMEAN, lse_atol=BF16_LSE_ATOL)
+    check_img_logits(g, out["img_logits"].cpu().numpy(), BF16_LOGIT_RTOL, case + " bf16", mean_rtol=BF16_LOGIT_MEAN,
+                     p99=BF16_LOGIT_P99, col_mean=BF16_LOGIT_COLMEAN)
     got = np.array([float(out[k]) for k in ("masked_lm_loss", "masked_img_loss", "masked_lm_loss_pv", "loss_lpm",
                                            "next_sentence_loss", "loss")])
     rel = np.abs(got - g["losses"]) / np.maximum(np.abs(g["losses"]), 1e-3)

@@ -9,6 +9,8 @@
   (1 - beta1) times the mean of the two micro-batch gradients;
 * NaN fail-fast on a batch with no masked region (the reference's 0/0 region loss).
 """
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -200,9 +202,17 @@ def test_nan_loss_fails_fast(dev):
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_overlapped_optimizer_bit_identical(dev, dtype):
     """The per-block AdamW on the side stream (Trainer.overlap, K3M_OPT_OVERLAP) updates every element exactly as
-    the one sweep after the backward (AdamW is elementwise; the blocks only re-cut the runs): parameters, both
-    moments, the bf16 shadow and the zeroed gradient are bit-identical after three steps, and every optimised
-    element is covered by exactly one block run."""
+    the one sweep after the backward (AdamW is elementwise; the blocks only re-cut the runs).
+
+    The backward itself is not bit-reproducible run to run (the structure aggregator's and the embedding
+    backward's float atomics, like the reference's index_add_ on the GPU), so the check is split in two:
+    * mechanics, bit-exact: the gradients each block's AdamW consumed are captured at hand-off; a twin trainer
+      restored to the same pre-step state runs the one sweep on exactly those gradients, and parameters, both
+      moments and the bf16 shadow agree bit for bit after each of three steps; every optimised element is
+      covered by exactly one block run; the gradient buffer is zero afterwards;
+    * hand-off timing: the captured gradients match a sweep run's final gradients to the run-to-run rounding
+      of the atomics (1e-3 of each tensor's max + 1e-8: the attention key biases' gradient is zero up to rounding), i.e. no block was read before the backward finished it (fp32 only: with a bf16 encoder the atomics'
+      rounding flips bf16 roundings downstream, 0.5% of a tensor's max run to run; the hand-offs are the same)."""
     from k3m_amd.trainer import Trainer
     from k3m_amd.synthetic import synthetic_batch, synthetic_noise
     cfg = _no_dropout_cfg()
@@ -210,26 +220,64 @@ def test_overlapped_optimizer_bit_identical(dev, dtype):
     batches = [synthetic_batch(cfg, B, dev, seed=s) for s in (41, 42, 43)]
     noises = [{k: v.to(dev) for k, v in synthetic_noise(cfg, B, seed=s).items()} for s in (51, 52, 53)]
     ent, val = _fixed_negs(B, 20, 10)
-    res = []
-    for overlap in (False, True):
+
+    def mk(overlap):
         tr = Trainer(cfg, dev, lr=1e-3, warmup_steps=1, total_steps=10, seed=5, dtype=dtype, nan_check=False)
         tr.overlap = overlap
-        for b, nz in zip(batches, noises):
-            tr.step(b, noise=nz, ent_neg=ent, val_neg=val)
+        return tr
+
+    ta, tb, tc = mk(True), mk(False), mk(False)
+    fa, fb, fc = ta.engine.fp, tb.engine.fp, tc.engine.fp
+    cap = torch.zeros_like(fa.grad)
+    orig = ta._overlap_block
+
+    def capture(blk):
+        if blk in ta._pending:
+            for a, n, _, _ in ta.block_runs[blk]:
+                cap[a:a + n].copy_(fa.grad[a:a + n])   # before orig() records the hand-off event
+        orig(blk)
+    ta._overlap_block = capture
+    final_c = []
+    orig_c = tc.optimizer_step
+
+    def grab(*a, **k):
+        final_c.append(fc.grad.clone())
+        return orig_c(*a, **k)
+    tc.optimizer_step = grab
+    for k, (b, nz) in enumerate(zip(batches, noises)):
+        pre = (fa.data.clone(), ta.m.clone(), ta.v.clone(), fa.data16.clone() if fa.data16 is not None else None)
+        ta.step(b, noise=nz, ent_neg=ent, val_neg=val)
+        tc.step(b, noise=nz, ent_neg=ent, val_neg=val)
+        fb.data.copy_(pre[0])
+        tb.m.copy_(pre[1])
+        tb.v.copy_(pre[2])
+        if pre[3] is not None:
+            fb.data16.copy_(pre[3])
+        fb.shadow_fresh = fa.shadow_fresh
+        tb.global_step = k
+        fb.grad.copy_(cap)
+        tb.optimizer_step()
         torch.cuda.synchronize()
-        fp = tr.engine.fp
-        res.append((fp.data.clone(), tr.m.clone(), tr.v.clone(),
-                    fp.data16.clone() if fp.data16 is not None else None, float(fp.grad.abs().max()), tr))
-    (p0, m0, v0, s0, g0, t0), (p1, m1, v1, s1, g1, t1) = res
-    assert t1.global_step == 3 and g0 == 0.0 and g1 == 0.0
-    assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
-    if s0 is not None:
-        assert torch.equal(s0, s1)
-    cover = torch.zeros(p0.numel(), dtype=torch.int32)
-    for runs in t1.block_runs.values():
+        assert ta.global_step == k + 1 and float(fa.grad.abs().max()) == 0.0
+        assert torch.equal(fa.data, fb.data), k
+        assert torch.equal(ta.m, tb.m) and torch.equal(ta.v, tb.v), k
+        if fa.data16 is not None:   # over the optimised runs (the forward refreshes the rest of the shadow)
+            for a, n, _, _ in ta.runs:
+                assert torch.equal(fa.data16[a:a + n], fb.data16[a:a + n]), (k, a, n)
+        bad = []
+        for name, shape in (fa.spec if dtype == "fp32" else ()):
+            o = fa.offsets[name]
+            n = math.prod(shape)
+            x, y = cap[o:o + n], final_c[k][o:o + n]
+            tol = 1e-3 * float(y.abs().max()) + 1e-8   # key biases: gradient zero up to rounding
+            if float((x - y).abs().max()) > tol:
+                bad.append((name, float((x - y).abs().max()), tol))
+        assert not bad, (k, bad[:10])
+    cover = torch.zeros(fa.data.numel(), dtype=torch.int32)
+    for runs in ta.block_runs.values():
         for a, n, _, _ in runs:
             cover[a:a + n] += 1
     whole = torch.zeros_like(cover)
-    for a, n, _, _ in t1.runs:
+    for a, n, _, _ in ta.runs:
         whole[a:a + n] = 1
     assert int(cover.max()) == 1 and torch.equal(cover.bool(), whole.bool())
