@@ -59,3 +59,42 @@ if len(sys.argv) > 4:
     print("\ntop (kernel, grid) classes")
     for (k, g), (t, c) in sorted(cls.items(), key=lambda kv: -kv[1][0])[:int(sys.argv[4])]:
         print("%-70s %-28s %4d/step %7.3f ms/step  %7.1f us avg" % (k, g, c // steps, t / 1e6 / steps, t / 1e3 / c))
+
+# optimizer time NOT hidden behind other kernels (the per-block AdamW runs on a side stream): the length of
+# the union of adamw intervals minus its intersection with the union of every other kernel's intervals
+
+
+def _union(iv):
+    out = []
+    for s, e in sorted(iv):
+        if out and s <= out[-1][1]:
+            out[-1][1] = max(out[-1][1], e)
+        else:
+            out.append([s, e])
+    return out
+
+
+def _length(iv):
+    return sum(e - s for s, e in iv)
+
+
+def _intersect(a, b):
+    out, i, j = [], 0, 0
+    while i < len(a) and j < len(b):
+        s, e = max(a[i][0], b[j][0]), min(a[i][1], b[j][1])
+        if s < e:
+            out.append([s, e])
+        if a[i][1] < b[j][1]:
+            i += 1
+        else:
+            j += 1
+    return out
+
+
+adam = _union([(s, e) for s, e, name in ev if s >= t0 and "adamw" in name])
+other = _union([(s, e) for s, e, name in ev if s >= t0 and "adamw" not in name])
+if adam:
+    busy_adam = _length(adam)
+    exposed = busy_adam - _length(_intersect(adam, other))
+    print("\nAdamW: %.3f ms/step of kernel-union time, %.3f ms/step exposed (not overlapped by another kernel)" % (
+        busy_adam / 1e6 / steps, exposed / 1e6 / steps))
