@@ -40,6 +40,7 @@ sys.path.insert(0, HERE)
 BASELINE_METRIC = "pretrain samples/sec/GPU (bert_base_6layer_6conect, bs=64) at 1/2/4/8 MI355X"
 PEAK_F32_MFMA = 157.3e12      # MI355X f32 MFMA dense peak (MI355X_MICROARCH.md)
 PEAK_BF16_MFMA = 2.5e15
+PROBE_STEPS = 2   # eager steps that carry the HIP-event probes when the timed steps are graph replays
 PEAK_F32_X6 = PEAK_BF16_MFMA / 6   # fp32 GEMM as 6 bf16 MFMA partial products (gemm_x6_tile.h)
 
 # BASELINE.json configs -> synthetic workload shapes
@@ -84,6 +85,8 @@ def parse():
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL) for real runs; gloo only to rehearse the "
                     "multi-rank path with several ranks sharing one GPU")
     ap.add_argument("--master-port", type=int, default=0)
+    ap.add_argument("--graph", default=None, choices=["auto", "on", "off"],
+                    help="hipGraph replay of the step (k3m_amd/graph.py); default: K3M_GRAPH (auto)")
     ap.add_argument("--ddp", action="store_true", help="run the data-parallel path (process group, bucketed "
                     "all-reduce on the comm stream) even at one rank: exercises RCCL at world size 1")
     return ap.parse_args()
@@ -324,6 +327,8 @@ def main():
     cfg = pretrain_config(os.path.join(HERE, "configs", "bert_base_6layer_6conect.json"))
     tr = Trainer(cfg, dev, lr=1e-4, warmup_steps=max(1, (args.steps + args.warmup) // 10),
                  total_steps=10 * (args.steps + args.warmup), seed=1234, init=True, dtype=dtype)
+    if args.graph is not None:
+        tr.graph = {"auto": "auto", "on": True, "off": False}[args.graph]
     if use_dist:
         ddp = GradAllReducer(tr.engine.fp, comm_dtype=torch.bfloat16 if dtype == "bf16" else None)
         ddp.broadcast_params(tr.engine.fp)
@@ -342,10 +347,17 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
+    # a repeated step may be replayed as one hipGraph (k3m_amd/graph.py): its first sighting runs eagerly, the
+    # second is timed and the third decides (and captures): three untimed steps keep that out of the timed region
+    warm = max(args.warmup, 3) if (tr.graph and not use_dist) else args.warmup
+    for _ in range(warm):
         tr.step(batch)
     barrier()
-    probe.active = cprobe.active = True
+    # the GEMM / co-attention HIP-event probes bracket Python-issued launches: live in the timed region when the
+    # step is issued eagerly; with graph replay (a captured launch cannot be bracketed by timing events) they
+    # run in PROBE_STEPS eager steps right after it (same kernels, same shapes)
+    graphed = tr.graph and tr._graphs is not None and tr._graphs.graph is not None
+    probe.active = cprobe.active = not graphed
     t0 = time.perf_counter()
     host = 0.0
     for _ in range(args.steps):
@@ -354,6 +366,7 @@ def main():
         host += time.perf_counter() - h0
     barrier()
     dt = time.perf_counter() - t0
+    loss = float(out["loss"])   # the last timed step's (a replay's outputs are overwritten by the next)
     probe.active = cprobe.active = False
     per_rank = [dt]
     if use_dist:
@@ -362,8 +375,25 @@ def main():
         dist.all_gather(gl, t)
         per_rank = [float(x) for x in gl]
         dt = max(per_rank)
+    # host issue cost from an idle GPU (the timed loop's host time includes blocking on a full launch queue)
+    issue = []
+    for _ in range(2):
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        tr.step(batch)
+        issue.append(time.perf_counter() - h0)
+    barrier()
+    probe_steps = args.steps
+    if graphed:
+        probe_steps = PROBE_STEPS
+        mode, tr.graph = tr.graph, False
+        probe.active = cprobe.active = True
+        for _ in range(probe_steps):
+            tr.step(batch)
+        barrier()
+        probe.active = cprobe.active = False
+        tr.graph = mode
     tr.finish()
-    loss = float(out["loss"])
     ms_step = 1000.0 * dt / args.steps
     value = world * B * args.steps / dt
     gemm_ms = probe.mean_ms()
@@ -378,10 +408,10 @@ def main():
     traffic, traffic_src = pmc_traffic(probe.key, kname)
     ref_sample = 3.0 * ref_fwd_flops(T, P, R, shape["n_triples"])
     co_flops = 3.0 * coattn_fwd_flops(T, P, R) * B
-    co_ms = cprobe.total_ms() / args.steps if cprobe.events else None
+    co_ms = cprobe.total_ms() / probe_steps if cprobe.events else None
     res = {
         "metric": BASELINE_METRIC,
-        "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": warm,
         "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": dtype, "data": "synthetic (SURVEY §8(d): random token ids, %dx2048 region feats, %d PV triples)" % (
             shape["nbox"], shape["n_triples"]),
@@ -394,6 +424,12 @@ def main():
         # host time to issue one step (Python engine + launches; the GPU runs behind it): when this
         # approaches ms_per_step the step is launch-bound and the GPU idles between kernels
         "host_ms_per_step": round(1000.0 * host / args.steps, 3),
+        # the same, each step issued from an idle GPU (two extra untimed steps): the Python engine's own cost
+        "host_issue_ms": round(1000.0 * min(issue), 3),
+        # the step's issue mode: K3M_GRAPH auto replays a hipGraph when the eager issue time is a large share of
+        # the GPU time (decision: the measured eager step); captures / replays count graph launches
+        "graph": ({"captures": tr._graphs.captures, "replays": tr._graphs.replays,
+                   "decision": tr._graphs.last_decision} if tr._graphs is not None else None),
         "loss": round(loss, 4),
         "step_mfma_frac_vs_ref_flops": round(B * ref_sample / (ms_step * 1e-3) / peak, 4),
         "roofline": {"bound": "mfma", "kernel": "%s text-layer FFN1 %dx%dx%d" % (kname, Mg, Ng, Kg),
@@ -403,6 +439,8 @@ def main():
                      "traffic": traffic,
                      "avg_launch_ms": round(gemm_ms, 4) if gemm_ms else None,
                      "launches": len(probe.events),
+                     "probe": "HIP events, %s" % ("%d eager steps after the timed graph replays" % probe_steps if graphed
+                                                  else "timed region"),
                      "algorithmic_flops_per_launch": gemm_flops,
                      "peak_basis": ("bf16 dense MFMA" if bf else "fp32 via 6 bf16 MFMA partial products = bf16 dense "
                                     "peak / 6" if x6 else "f32 MFMA"),

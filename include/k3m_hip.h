@@ -280,6 +280,22 @@ int k3m_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, lo
 int k3m_adamw_ex(float* p, float* g, float* m, float* v, uint16_t* p_bf16, long long n, double lr, double beta1,
                  double beta2, double eps, double wd, int step, float grad_scale, int flags, hipStream_t stream);
 
+/* Whole-step hipGraph replay (k3m_amd/graph.py; no reference counterpart — the reference re-issues
+ * every launch from Python each step, train_concap_struc.py:466-589).  A captured launch keeps its
+ * by-value arguments, so the two per-step values come from device memory:
+ *  - k3m_adamw_ex_dev: k3m_adamw_ex whose four derived fp32 scalars (step_size, decay, 1/bc1, 1/bc2)
+ *    are read from `scalars` (16-B aligned device memory) when the kernel runs;
+ *    k3m_adamw_scalars_n writes, for n (lr[i], wd[i]) pairs, exactly the four values k3m_adamw_ex
+ *    would pass for (lr[i], beta1, beta2, wd[i], step, flags) (host memory, out[4*i .. 4*i+3]);
+ *  - seeds: a launch whose seed has bit 63 set (K3M_GRAPH_SEED; host seeds are below 2^63) draws
+ *    with the 64-bit seed stored at device address (seed & ~K3M_GRAPH_SEED) when it runs (every
+ *    dropout / gumbel / sampling kernel of this library). */
+#define K3M_GRAPH_SEED (1ull << 63)
+int k3m_adamw_ex_dev(float* p, float* g, float* m, float* v, uint16_t* p_bf16, long long n, const float* scalars,
+                     double beta1, double beta2, double eps, float grad_scale, int flags, hipStream_t stream);
+int k3m_adamw_scalars_n(int n, const double* lr, const double* wd, double beta1, double beta2, int step, int flags,
+                        float* out);
+
 /* Attention for sequences longer than 128 (up to 512 keys, d <= 128): the fine-tuning PV text
  * (max_seq_length_pv 256, finetune.py:1275) and SURVEY config 5 (P = 320).  Same arguments,
  * semantics, probability layout and dropout counters as k3m_attn_fwd / k3m_attn_bwd; the backward

@@ -20,6 +20,7 @@ GEMM_SLABS_ONLY = 0x100   # K3M_GEMM_SLABS_ONLY: split-K slabs left for k3m_slab
 GEMM_COLSUM_SLABS = 0x200   # K3M_GEMM_COLSUM_SLABS: dGELU output column sums as 32-row slabs in ws
 F32_SPLIT_BF16X6, F32_MFMA_F32 = 0, 1
 ADAM_ZERO_GRAD, ADAM_APEX, ADAM_APEX_BIAS_CORRECTION = 1, 2, 4
+GRAPH_SEED = 1 << 63   # K3M_GRAPH_SEED | address: the kernels read the seed from that device word
 
 vp, i32, i64, f32, u64 = C.c_void_p, C.c_int, C.c_longlong, C.c_float, C.c_uint64
 
@@ -77,6 +78,8 @@ SIGNATURES = {
     "k3m_adamw": [vp, vp, vp, vp, vp, i64, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double, i32, f32, vp],
     "k3m_adamw_ex": [vp, vp, vp, vp, vp, i64, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double, i32, f32,
                      i32, vp],
+    "k3m_adamw_ex_dev": [vp, vp, vp, vp, vp, i64, vp, C.c_double, C.c_double, C.c_double, f32, i32, vp],
+    "k3m_adamw_scalars_n": [i32, vp, vp, C.c_double, C.c_double, i32, i32, vp],
     "k3m_cast_f32_bf16": [vp, vp, i64, vp],
     "k3m_convert": [vp, i32, vp, i32, i64, i32, f32, vp],
     "k3m_add_inplace": [vp, vp, i64, f32, i32, vp],

@@ -85,7 +85,14 @@ __global__ __launch_bounds__(256) void adamw_ex_kernel(float* __restrict__ p, fl
                                                        float* __restrict__ m, float* __restrict__ v,
                                                        uint16_t* __restrict__ pb, long long n4, float b1, float omb1,
                                                        float b2, float omb2, float eps, float step_size, float decay,
-                                                       float gscale, float rbc1, float rbc2) {
+                                                       float gscale, float rbc1, float rbc2,
+                                                       const float* __restrict__ sc) {
+  if (sc) {   // k3m_adamw_ex_dev: the step's scalars from device memory (a hipGraph-captured launch)
+    step_size = sc[0];
+    decay = sc[1];
+    rbc1 = sc[2];
+    rbc2 = sc[3];
+  }
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
     floatx4 pp = reinterpret_cast<floatx4*>(p)[i];
     floatx4 gg = reinterpret_cast<const floatx4*>(g)[i];
@@ -121,18 +128,10 @@ __global__ __launch_bounds__(256) void adamw_ex_kernel(float* __restrict__ p, fl
 
 }  // namespace
 
-extern "C" int k3m_adamw_ex(float* p, float* g, float* m, float* v, uint16_t* p_bf16, long long n, double lr,
-                            double beta1, double beta2, double eps, double wd, int step, float grad_scale, int flags,
-                            hipStream_t st) {
-  K3M_ARG(p && g && m && v && n >= 0 && n % 4 == 0 && step >= 1);
-  K3M_ARG(((uintptr_t)p & 15) == 0 && ((uintptr_t)g & 15) == 0 && ((uintptr_t)m & 15) == 0 && ((uintptr_t)v & 15) == 0);
-  K3M_ARG((flags & ~(K3M_ADAM_ZERO_GRAD | K3M_ADAM_APEX | K3M_ADAM_APEX_BIAS_CORRECTION)) == 0);
-  if (n == 0) return 0;
-  const long long n4 = n / 4;
-  const int blocks = (int)std::min<long long>((n4 + 255) / 256, 256 * 16);
-  const bool apex = (flags & K3M_ADAM_APEX) != 0, zero = (flags & K3M_ADAM_ZERO_GRAD) != 0;
+// (step_size, decay, 1/bc1, 1/bc2) of one k3m_adamw_ex launch, in double on the host, rounded once
+static void adam_scalars(double lr, double beta1, double beta2, double wd, int step, int flags, float* out) {
   float step_size, decay, rbc1 = 1.f, rbc2 = 1.f;
-  if (apex) {
+  if (flags & K3M_ADAM_APEX) {
     if (flags & K3M_ADAM_APEX_BIAS_CORRECTION) {
       rbc1 = (float)(1.0 / (1.0 - std::pow(beta1, step)));
       rbc2 = (float)(1.0 / (1.0 - std::pow(beta2, step)));
@@ -144,10 +143,26 @@ extern "C" int k3m_adamw_ex(float* p, float* g, float* m, float* v, uint16_t* p_
     step_size = (float)(lr * std::sqrt(bc2) / bc1);
     decay = wd > 0.0 ? (float)(lr * wd) : 0.f;
   }
+  out[0] = step_size;
+  out[1] = decay;
+  out[2] = rbc1;
+  out[3] = rbc2;
+}
+
+static int adamw_ex_launch(float* p, float* g, float* m, float* v, uint16_t* p_bf16, long long n, const float* s4,
+                           const float* dev_sc, double beta1, double beta2, double eps, float grad_scale, int flags,
+                           hipStream_t st) {
+  K3M_ARG(p && g && m && v && n >= 0 && n % 4 == 0);
+  K3M_ARG(((uintptr_t)p & 15) == 0 && ((uintptr_t)g & 15) == 0 && ((uintptr_t)m & 15) == 0 && ((uintptr_t)v & 15) == 0);
+  K3M_ARG((flags & ~(K3M_ADAM_ZERO_GRAD | K3M_ADAM_APEX | K3M_ADAM_APEX_BIAS_CORRECTION)) == 0);
+  if (n == 0) return 0;
+  const long long n4 = n / 4;
+  const int blocks = (int)std::min<long long>((n4 + 255) / 256, 256 * 16);
+  const bool apex = (flags & K3M_ADAM_APEX) != 0, zero = (flags & K3M_ADAM_ZERO_GRAD) != 0;
 #define K3M_ADAM_LAUNCH(A, Z)                                                                                      \
   hipLaunchKernelGGL((adamw_ex_kernel<A, Z>), dim3(blocks), dim3(256), 0, st, p, g, m, v, p_bf16, n4, (float)beta1, \
-                     (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps, step_size, decay,         \
-                     grad_scale, rbc1, rbc2)
+                     (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps, s4[0], s4[1], grad_scale,  \
+                     s4[2], s4[3], dev_sc)
   if (apex) {
     if (zero) K3M_ADAM_LAUNCH(true, true);
     else K3M_ADAM_LAUNCH(true, false);
@@ -157,6 +172,31 @@ extern "C" int k3m_adamw_ex(float* p, float* g, float* m, float* v, uint16_t* p_
   }
 #undef K3M_ADAM_LAUNCH
   K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_adamw_ex(float* p, float* g, float* m, float* v, uint16_t* p_bf16, long long n, double lr,
+                            double beta1, double beta2, double eps, double wd, int step, float grad_scale, int flags,
+                            hipStream_t st) {
+  K3M_ARG(step >= 1);
+  float s4[4];
+  adam_scalars(lr, beta1, beta2, wd, step, flags, s4);
+  return adamw_ex_launch(p, g, m, v, p_bf16, n, s4, nullptr, beta1, beta2, eps, grad_scale, flags, st);
+}
+
+extern "C" int k3m_adamw_ex_dev(float* p, float* g, float* m, float* v, uint16_t* p_bf16, long long n,
+                                const float* scalars, double beta1, double beta2, double eps, float grad_scale,
+                                int flags, hipStream_t st) {
+  K3M_ARG(scalars && ((uintptr_t)scalars & 15) == 0);
+  const float zero4[4] = {0.f, 0.f, 0.f, 0.f};
+  return adamw_ex_launch(p, g, m, v, p_bf16, n, zero4, scalars, beta1, beta2, eps, grad_scale, flags, st);
+}
+
+extern "C" int k3m_adamw_scalars_n(int n, const double* lr, const double* wd, double beta1, double beta2, int step,
+                                   int flags, float* out) {
+  K3M_ARG(n >= 0 && (n == 0 || (lr && wd && out)) && step >= 1);
+  K3M_ARG((flags & ~(K3M_ADAM_ZERO_GRAD | K3M_ADAM_APEX | K3M_ADAM_APEX_BIAS_CORRECTION)) == 0);
+  for (int i = 0; i < n; ++i) adam_scalars(lr[i], beta1, beta2, wd[i], step, flags, out + 4 * i);
   return 0;
 }
 

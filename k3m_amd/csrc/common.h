@@ -38,6 +38,16 @@ template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float v) {
 // Stateless: every dropout / gumbel site draws u(seed, offset + element) so the backward pass
 // regenerates the forward mask instead of storing it.
 //
+// hipGraph replay (k3m_amd/graph.py): a captured launch keeps the by-value seed it was captured with,
+// so a captured step passes seed = K3M_GRAPH_SEED | (device address of a 64-bit word) and every draw
+// reads the step's seed from that word, which the host refills before each replay.  Host seeds are
+// 63-bit, so eager launches (bit 63 clear) are unchanged.  Resolved inside k3m_seed_key, through
+// which every draw goes.
+__device__ __forceinline__ uint64_t k3m_seed_resolve(uint64_t seed) {
+  if (seed & K3M_GRAPH_SEED) seed = *reinterpret_cast<const uint64_t*>(seed & ~K3M_GRAPH_SEED);
+  return seed;
+}
+//
 // Cost matters: the attention softmax and LayerNorm tails draw one value per element.  The 64-bit
 // seed is expanded once per launch (splitmix64 of a kernel argument: wave-uniform, scalar ALU);
 // per element the counter's high word is folded in with one multiply and the low word goes
@@ -52,7 +62,7 @@ __device__ __forceinline__ uint32_t k3m_mix32(uint32_t x) {
   return x;
 }
 __device__ __forceinline__ uint64_t k3m_seed_key(uint64_t seed) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull;
+  uint64_t z = k3m_seed_resolve(seed) + 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);

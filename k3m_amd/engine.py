@@ -495,6 +495,12 @@ class K3MEngine(object):
         fp = self.fp = FlatParams(cfg, self.device, bf16_shadow=(dtype == "bf16"))
         self.base_seed = int(seed)
         self.step_count = 0
+        # hipGraph capture (k3m_amd/graph.py): graph_seed = device address of the seed word the replay refills;
+        # launches then pass K3M_GRAPH_SEED | address and draw with that word's value.  The label-count check
+        # is left to the replay (no host work inside a capture).
+        self.graph_seed = 0
+        self.capturing = False
+        self.captured_counts = None
         # tests: keep copies of the labelled-row MLM logits and masked-region logits of each forward
         # (out["mlm_logits"] rows in compaction order — text rows, then PV rows, row-major; out["img_logits"])
         self.capture_logits = False
@@ -577,6 +583,10 @@ class K3MEngine(object):
         self._hint_checks.append((tuple(hint), host, ev))
         self.check_hints()
 
+    def step_seed(self, seed):
+        """The 63-bit seed forward(seed=seed) draws with (the word a graph replay writes)."""
+        return Rng(self.base_seed * 1000003 + seed).seed
+
     def check_hints(self, wait=False):
         pend = getattr(self, "_hint_checks", [])
         while pend and (wait or pend[0][2].query()):
@@ -610,6 +620,8 @@ class K3MEngine(object):
         R = feat.shape[1]
         BT, BP, BR = B * T, B * P, B * R
         rng = Rng(self.base_seed * 1000003 + (seed if seed is not None else self.step_count))
+        if self.graph_seed:
+            rng.seed = L.GRAPH_SEED | int(self.graph_seed)
         ph = self.p_h if train else 0.0
         pvh = self.p_vh if train else 0.0
         ctx = {"B": B, "T": T, "P": P, "R": R, "train": train, "seed": rng.seed}
@@ -861,7 +873,10 @@ class K3MEngine(object):
         hint = batch.get("_label_counts")
         if hint is not None:   # counted on the host when the batch was built (label_counts): no sync
             n_m, n_v = int(hint[0]), int(hint[1])
-            self._verify_hint((n_m, n_v), cnt)
+            if self.capturing:
+                self.captured_counts = cnt   # checked by the graph after each replay
+            else:
+                self._verify_hint((n_m, n_v), cnt)
         else:
             n_m, n_v = [int(x) for x in cnt.tolist()]   # host sync (labelled-row counts)
 

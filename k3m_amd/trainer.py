@@ -145,6 +145,10 @@ def block_runs(fp, weight_decay=0.01, lr_mult=None, frozen_names=()):
 # process, no gradient accumulation pending): the HBM-bound sweep overlaps the rest of the backward instead of
 # following it.  K3M_OPT_OVERLAP=0 restores the one sweep after the backward.
 OPT_OVERLAP = os.environ.get("K3M_OPT_OVERLAP", "1") != "0"
+# Replay a repeated step as one hipGraph (k3m_amd/graph.py): "auto" (default) when the eager step's host issue
+# time is a large share of its GPU time, "1" always, "0" never (every launch issued from Python).
+_g = os.environ.get("K3M_GRAPH", "auto")
+GRAPH_STEP = "auto" if _g == "auto" else _g != "0"
 
 
 class LossWatch(object):
@@ -232,6 +236,9 @@ class Trainer(object):
         self.block_runs = block_runs(fp, weight_decay, lr_mult, frozen_names)
         self.opt_stream = None
         self.overlap = OPT_OVERLAP
+        self.graph = GRAPH_STEP
+        self._graphs = None
+        self._adam_table = None   # set while a hipGraph captures the step (k3m_amd/graph.py)
 
     def evaluate(self, batch, noise=None, ent_neg=None, val_neg=None):
         """The validation forward of train_concap_struc.py:612-688 (model.eval(), no gradients): returns
@@ -259,15 +266,25 @@ class Trainer(object):
         return mult * self.current_lr()
 
     # ---------------------------------------------------------------- optimizer
-    def _adam_runs(self, runs, step, grad_scale, flags):
+    def _adamw(self, off, n, wd, mult, step, grad_scale, flags):
+        """k3m_adamw_ex over one run; inside a hipGraph capture k3m_adamw_ex_dev with the run's row of the
+        graph's scalar table (k3m_amd/graph.py refills it before each replay)."""
         fp = self.engine.fp
+        # with a bf16 encoder the same launch refreshes the weight shadow from the new fp32 values
+        sh = fp.data16[off:].data_ptr() if fp.data16 is not None else None
+        if self._adam_table is not None:
+            row = self._adam_table.row(mult, wd, flags)   # lr = mult * current_lr(): warmup_linear only
+            L.call("k3m_adamw_ex_dev", fp.data[off:].data_ptr(), fp.grad[off:].data_ptr(), self.m[off:].data_ptr(),
+                   self.v[off:].data_ptr(), sh, n, row, self.beta1, self.beta2, self.eps, grad_scale, flags, L.stream())
+            return
+        L.call("k3m_adamw_ex", fp.data[off:].data_ptr(), fp.grad[off:].data_ptr(), self.m[off:].data_ptr(),
+               self.v[off:].data_ptr(), sh, n, self.run_lr(off, mult), self.beta1, self.beta2, self.eps, wd, step,
+               grad_scale, flags, L.stream())
+
+    def _adam_runs(self, runs, step, grad_scale, flags):
         for off, n, wd, mult in runs:
-            if n == 0:
-                continue
-            sh = fp.data16[off:].data_ptr() if fp.data16 is not None else None
-            L.call("k3m_adamw_ex", fp.data[off:].data_ptr(), fp.grad[off:].data_ptr(), self.m[off:].data_ptr(),
-                   self.v[off:].data_ptr(), sh, n, self.run_lr(off, mult), self.beta1, self.beta2, self.eps, wd, step,
-                   grad_scale, flags, L.stream())
+            if n:
+                self._adamw(off, n, wd, mult, step, grad_scale, flags)
 
     def _overlap_begin(self):
         """State of an overlapped optimizer step: blocks still to update and the side stream."""
@@ -292,7 +309,7 @@ class Trainer(object):
         self._overlap_block(("head", 0))
         self._overlap_block((kind, index))
 
-    def _overlap_finish(self):
+    def _overlap_finish(self, count=True):
         fp = self.engine.fp
         fresh = fp.shadow_fresh
         for blk in sorted(self._pending):
@@ -301,10 +318,12 @@ class Trainer(object):
         for name in self.excluded:   # --freeze: gradients the optimizer skips are dropped as well
             fp.g[name].zero_()
         fp.shadow_fresh = fresh
-        self.global_step += 1
+        if count:
+            self.global_step += 1
 
-    def optimizer_step(self, grad_scale=1.0, zero_grad=True):
-        """One optimizer step over every run; the gradient buffer is zeroed in the same sweep."""
+    def optimizer_step(self, grad_scale=1.0, zero_grad=True, count=True):
+        """One optimizer step over every run; the gradient buffer is zeroed in the same sweep.
+        count=False (a graph capture): the step counter is left to the replay."""
         fp = self.engine.fp
         step = self.global_step + 1
         fresh = fp.shadow_fresh
@@ -312,23 +331,21 @@ class Trainer(object):
         for off, n, wd, mult in self.runs:
             if n == 0:
                 continue
-            # with a bf16 encoder the same launch refreshes the weight shadow from the new fp32 values
-            sh = fp.data16[off:].data_ptr() if fp.data16 is not None else None
             if self.ADAMW is not None:   # torch.optim.AdamW (fine-tuning); zeroing below
+                sh = fp.data16[off:].data_ptr() if fp.data16 is not None else None
                 L.call(self.ADAMW, fp.data[off:].data_ptr(), fp.grad[off:].data_ptr(), self.m[off:].data_ptr(),
                        self.v[off:].data_ptr(), sh, n, self.run_lr(off, mult), self.beta1, self.beta2, self.eps, wd,
                        step, grad_scale, L.stream())
                 continue
-            L.call("k3m_adamw_ex", fp.data[off:].data_ptr(), fp.grad[off:].data_ptr(), self.m[off:].data_ptr(),
-                   self.v[off:].data_ptr(), sh, n, self.run_lr(off, mult), self.beta1, self.beta2, self.eps, wd, step,
-                   grad_scale, flags, L.stream())
+            self._adamw(off, n, wd, mult, step, grad_scale, flags)
         if zero_grad and self.ADAMW is not None:
             fp.grad.zero_()
         elif zero_grad:
             for name in self.excluded:   # --freeze: gradients the optimizer skips are dropped as well
                 fp.g[name].zero_()
         fp.shadow_fresh = fresh   # frozen tensors are not updated: the shadow stays as fresh as it was
-        self.global_step += 1
+        if count:
+            self.global_step += 1
 
     def finish(self):
         """Synchronising end-of-run (or end-of-epoch) checks: every outstanding label-count hint and
@@ -351,7 +368,42 @@ class Trainer(object):
     # ---------------------------------------------------------------- the step
     def step(self, batch, noise=None, ent_neg=None, val_neg=None):
         """One micro-step (forward + backward); the optimizer runs every ``accum_steps`` calls.
-        Returns the forward's outputs; ``out["loss"]`` is the optimised objective."""
+        Returns the forward's outputs; ``out["loss"]`` is the optimised objective.
+
+        With ``self.graph`` (K3M_GRAPH: True, or "auto" = when the step is host-bound) a step that a hipGraph can
+        replay (k3m_amd/graph.py: one process, no accumulation, host label counts, the default schedule) runs as
+        one graph launch once the same batch shapes repeat; its outputs are then the graph's static tensors,
+        overwritten by the next replay."""
+        if self.graph and noise is None and ent_neg is None and val_neg is None:
+            if self._graphs is None:
+                from .graph import StepGraphs
+                self._graphs = StepGraphs(self)
+            out = self._graphs.step(batch)
+            if out is not None:
+                return out
+        return self._eager_step(batch, noise, ent_neg, val_neg)
+
+    def _device_step(self, batch):
+        """The device work of one optimizer step (forward, backward, AdamW) with no host-side bookkeeping:
+        the body a hipGraph captures.  Preconditions: single process, accum_steps == 1, a label-count hint."""
+        eng = self.engine
+        if self.objective == 1:
+            batch = objective1_labels(batch)
+        out, ctx = eng.forward(batch, train=self.dropout, seed=self.global_step)
+        out["loss"] = out["masked_lm_loss"] + out["masked_lm_loss_pv"] + out["loss_lpm"] + \
+            out["masked_img_loss"] * self.loss_img_weight
+        hook = None
+        if self.overlap:
+            self._overlap_begin()
+            hook = self._overlap_hook
+        eng.backward(ctx, w_mlm=1.0, w_img=self.loss_img_weight, w_lpm=1.0, grad_ready=hook)
+        if self.overlap:
+            self._overlap_finish(count=False)
+        else:
+            self.optimizer_step(count=False)
+        return out
+
+    def _eager_step(self, batch, noise=None, ent_neg=None, val_neg=None):
         eng = self.engine
         if self.objective == 1:
             batch = objective1_labels(batch)

@@ -1,0 +1,164 @@
+"""Whole-step hipGraph replay (k3m_amd/graph.py) against the eager step.
+
+* k3m_adamw_ex_dev with the row k3m_adamw_scalars_n wrote is bit-identical to k3m_adamw_ex (both AdamW
+  variants, with the bf16 shadow);
+* a dropout draw with seed K3M_GRAPH_SEED | (address of a device word holding S) equals the eager draw
+  with that seed, eagerly and inside a replayed graph whose word is refilled between replays;
+* the Trainer: a replayed step (dropout ON, both dtypes, the overlapped AdamW) from the same state as an
+  eager step gives the bit-identical loss (same parameters, same dropout masks), and the same update up
+  to the run-to-run rounding of the backward's float atomics (test_gpu_fullsize.py; two eager runs
+  differ the same way); one capture, the
+  following steps replayed.  Reference loop: train_concap_struc.py:466-589.
+"""
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import CFG_PATH
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda")
+
+
+@pytest.mark.parametrize("flags", [1, 1 | 2 | 4])
+def test_adamw_dev_scalars_bit_identical(dev, flags):
+    from k3m_amd import _lib as L
+    n = 4099 * 4
+    g0 = torch.Generator(device="cpu").manual_seed(3)
+    p = torch.randn(n, generator=g0).to(dev)
+    g = torch.randn(n, generator=g0).to(dev) * 1e-2
+    m = torch.randn(n, generator=g0).to(dev) * 1e-3
+    v = torch.rand(n, generator=g0).to(dev) * 1e-5
+    outs = []
+    for mode in ("host", "dev"):
+        pp, gg, mm, vv = p.clone(), g.clone(), m.clone(), v.clone()
+        sh = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+        lr, wd, step = 3e-4 * 0.1, 0.01, 7
+        if mode == "host":
+            L.call("k3m_adamw_ex", pp.data_ptr(), gg.data_ptr(), mm.data_ptr(), vv.data_ptr(), sh.data_ptr(), n, lr,
+                   0.9, 0.98, 1e-8, wd, step, 0.5, flags, L.stream())
+        else:
+            lr_a = np.array([lr], dtype=np.float64)
+            wd_a = np.array([wd], dtype=np.float64)
+            host = torch.empty((1, 4), dtype=torch.float32)
+            L.call("k3m_adamw_scalars_n", 1, lr_a.ctypes.data, wd_a.ctypes.data, 0.9, 0.98, step, flags,
+                   host.data_ptr())
+            row = host.to(dev)
+            L.call("k3m_adamw_ex_dev", pp.data_ptr(), gg.data_ptr(), mm.data_ptr(), vv.data_ptr(), sh.data_ptr(), n,
+                   row.data_ptr(), 0.9, 0.98, 1e-8, 0.5, flags, L.stream())
+        torch.cuda.synchronize()
+        outs.append((pp, gg, mm, vv, sh))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert float(outs[1][1].abs().max()) == 0.0   # K3M_ADAM_ZERO_GRAD
+
+
+def test_graph_seed_marker_draws_like_eager(dev):
+    from k3m_amd import _lib as L, ops
+    rows, cols = 257, 768
+    x = torch.randn(rows, cols, device=dev)
+    gam = torch.ones(cols, device=dev)
+    bet = torch.zeros(cols, device=dev)
+
+    def ln(seed):
+        y = torch.empty_like(x)
+        xh = torch.empty_like(x)
+        rs = torch.empty((rows,), device=dev)
+        ops.ln_fwd(x, None, gam, bet, y, xh, rs, p_out=0.1, seed=seed, off_out=12345)
+        return y
+    word = torch.zeros((1,), dtype=torch.int64, device=dev)
+    marker = L.GRAPH_SEED | word.data_ptr()
+    for s in (5, 987654321987):
+        eager = ln(s)
+        word.fill_(s)
+        marked = ln(marker)
+        torch.cuda.synchronize()
+        assert torch.equal(eager, marked), s
+        assert not torch.equal(eager, ln(s + 1))
+    # inside a graph: the captured launch keeps the marker; the word chooses the draw at replay time
+    g = torch.cuda.CUDAGraph()
+    word.fill_(0)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g):
+        y_static = ln(marker)
+    for s in (11, 12):
+        word.fill_(s)
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(y_static, ln(s)), s
+
+
+def _state(tr):
+    fp = tr.engine.fp
+    return (fp.data.clone(), tr.m.clone(), tr.v.clone(), fp.data16.clone() if fp.data16 is not None else None)
+
+
+def _load(tr, st):
+    fp = tr.engine.fp
+    fp.data.copy_(st[0])
+    tr.m.copy_(st[1])
+    tr.v.copy_(st[2])
+    if st[3] is not None:
+        fp.data16.copy_(st[3])
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_graph_step_matches_eager(dev, dtype):
+    from k3m_amd.config import pretrain_config
+    from k3m_amd.engine import label_counts
+    from k3m_amd.synthetic import synthetic_batch
+    from k3m_amd.trainer import Trainer
+    cfg = pretrain_config(CFG_PATH)
+    B = 4
+    batch = synthetic_batch(cfg, B, dev, seed=21)
+    batch["_label_counts"] = label_counts(batch)
+    lr = 1e-3
+    ta = Trainer(cfg, dev, lr=lr, warmup_steps=0, total_steps=20, seed=9, dtype=dtype)
+    tb = Trainer(cfg, dev, lr=lr, warmup_steps=0, total_steps=20, seed=9, dtype=dtype)
+    ta.graph, tb.graph = False, True
+    assert ta.dropout and tb.dropout
+    eager_ms, graph_ms = [], []
+    for k in range(4):
+        _load(tb, _state(ta))
+        tb.global_step = ta.global_step
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        la = float(ta.step(batch)["loss"])
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        ob = tb.step(batch)
+        t2 = time.perf_counter()
+        lb = float(ob["loss"])
+        eager_ms.append(1e3 * (t1 - t0))
+        graph_ms.append(1e3 * (t2 - t1))
+        assert la == lb, (k, la, lb)   # same parameters, same dropout masks: the forward is bitwise reproducible
+        assert ta.global_step == tb.global_step == k + 1
+        pa, pb = ta.engine.fp.data, tb.engine.fp.data
+        d = (pa - pb).abs()
+        mean_d, frac = float(d.mean()), float((d > 0.05 * lr).float().mean())
+        print("step %d: mean |dp| %.3e, fraction > 0.05 lr %.2e, max %.3e (lr %.0e)" % (k, mean_d, frac,
+                                                                                     float(d.max()), lr))
+        # updates of ~lr per element.  The atomics' rounding changes the Adam direction m/(sqrt(v)+eps) of the
+        # elements whose gradient is zero up to rounding (key biases, ~1e-4 of the parameters) by up to ~lr;
+        # a wrong learning rate, step or bias correction moves nearly every element by ~lr.  With a bf16 encoder a
+        # rounding difference upstream flips bf16 roundings downstream: two eager runs differ by 2.5e-3 lr on
+        # average there (measured), hence the wider bar
+        mean_bar, frac_bar = (1e-3, 1e-3) if dtype == "fp32" else (1e-2, 2e-2)
+        assert mean_d <= mean_bar * lr and frac <= frac_bar, (k, mean_d, frac)
+        assert float(tb.engine.fp.grad.abs().max()) == 0.0
+        if tb.engine.fp.data16 is not None:
+            ref16 = pb.to(torch.bfloat16)
+            assert torch.equal(tb.engine.fp.data16, ref16)
+    gs = tb._graphs
+    assert gs.captures == 1 and gs.replays == 3, (gs.captures, gs.replays)
+    tb.finish()
+    print("issue ms (host, step call): eager %s  graph %s" % (["%.1f" % x for x in eager_ms],
+                                                              ["%.1f" % x for x in graph_ms]))
