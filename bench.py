@@ -175,7 +175,9 @@ class CoattnProbe(object):
 def head_kernel(bf):
     """Full-name fragment of the kernel the probed GEMM runs at HEAD with the default knobs (gemm.hip /
     gemm_bf16.hip dispatch of a 256x256-tile problem of >= K3M_*_PERSIST_MIN blocks)."""
-    if bf:
+    if bf:   # FFN1 has the GELU epilogue: K3M_B16_DUAL (default 2) runs it on the two-workgroups-per-CU kernel
+        if os.environ.get("K3M_B16_DUAL", "2") != "0":
+            return "k3m_b16::gemm_dual_kernel<256, 128"
         return "k3m_b16::gemm_persist_kernel<256, 256" if os.environ.get("K3M_B16_PERSIST", "1") != "0" \
             else "k3m_b16::gemm_kernel<256, 256"
     return "k3m_x6::gemm_x6_persist_kernel<256, 256" if os.environ.get("K3M_X6_PERSIST", "1") != "0" \

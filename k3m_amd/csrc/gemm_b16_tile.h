@@ -121,6 +121,10 @@ struct Shape {
 template <int MF, int WTM, int WTN> struct Acc;
 template <int WTM, int WTN> struct Acc<16, WTM, WTN> {   // v_mfma_f32_16x16x32_bf16
   static constexpr int FM = WTM / 16, FN = WTN / 16;
+  // staging row stride = columns + PAD floats: the 4 row groups of one 16-lane write (rows 4g + r) land on
+  // 4 distinct 16-bank quarters (4 * PAD = 16 mod 64), and the 8-float row reads of the store pass (8 lanes per
+  // row) interleave two rows on the 64 banks — both conflict-free (PAD 8 put rows 4 apart on the same banks)
+  static constexpr int PAD = 4;
   floatx4 v[FM][FN];
   __device__ __forceinline__ void stage(int grp, float* wl, int ws, int lane) const {
 #pragma unroll
@@ -133,6 +137,7 @@ template <int WTM, int WTN> struct Acc<16, WTM, WTN> {   // v_mfma_f32_16x16x32_
 };
 template <int WTM, int WTN> struct Acc<32, WTM, WTN> {   // v_mfma_f32_32x32x16_bf16
   static constexpr int FM = WTM / 32, FN = WTN / 32;
+  static constexpr int PAD = 8;   // the two 32-lane halves of a write (rows 4 apart) on opposite bank halves
   floatx16 v[FM][FN];
   __device__ __forceinline__ void stage(int grp, float* wl, int ws, int lane) const {
 #pragma unroll
@@ -419,7 +424,7 @@ template <int TBM, int TBN, int WM, int WN, int EPI, typename CT, typename AccT,
 __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint16_t* smem_u16, const AccT& acc,
                                          int slice, Hook hook = Hook(), bool nostore = false) {
   using S = Shape<TBM, TBN, WM, WN>;
-  constexpr int WNC = TBN / WN, WS = WNC + 8, LPR = WNC / 8, RPP = 64 / LPR, NPS = 32 / RPP, NG = TBM / WM / 32;
+  constexpr int WNC = TBN / WN, WS = WNC + AccT::PAD, LPR = WNC / 8, RPP = 64 / LPR, NPS = 32 / RPP, NG = TBM / WM / 32;
   constexpr int RING = sizeof(CT) == 2 ? 2 : 1;   // passes the per-pass loads run ahead (register budget)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = (w / WN) * (TBM / WM), wn = (w % WN) * WNC;
