@@ -213,6 +213,8 @@ def linear_dgrad(dy, W, dx=None, beta=0.0, dgelu_aux=None, alpha=1.0, colsum_out
 # relative cost per extra split-K slice (its slab write + read), fp32 / bf16 weight gradients (A/B knobs)
 SPLITK_COST_F32 = float(os.environ.get("K3M_SPLITK_COST_F32", "0.01"))
 SPLITK_COST_BF16 = float(os.environ.get("K3M_SPLITK_COST_BF16", "0.02"))
+# fewest k rows per split-K slice of an fp32 weight gradient (A/B knob)
+SPLITK_MINK_F32 = int(os.environ.get("K3M_SPLITK_MINK_F32", "1024"))
 
 
 def _splitk(m, n, k, dtype=torch.float32):
@@ -225,7 +227,7 @@ def _splitk(m, n, k, dtype=torch.float32):
             return 1
         # minimise (waves of 256 blocks) x (k per split), plus ~1% per split for the slab reduction
         best, best_cost = 1, float("inf")
-        for s in range(1, min(32, k // 1024) + 1):
+        for s in range(1, min(32, k // SPLITK_MINK_F32) + 1):
             cost = ((tiles * s + 255) // 256) / s * (1.0 + SPLITK_COST_F32 * s)
             if cost < best_cost - 1e-9:
                 best, best_cost = s, cost
