@@ -21,7 +21,9 @@ MI355X:
 * every step records HIP events around each bucket on the comm stream plus one at the end of the
   backward on the compute stream: ``timing()`` reports the exposed all-reduce time (end of the last
   all-reduce minus end of the backward, 0 if hidden) and the comm stream's busy time, read after the
-  timed region (no host sync inside the step).
+  timed region (no host sync inside the step);
+* ``on_reduced`` (set by the Trainer): each block's AdamW is released from the comm stream as soon as the
+  block's buckets are reduced, on the optimizer's side stream.
 """
 import collections
 
@@ -84,6 +86,9 @@ class GradAllReducer(object):
         self.stream = None
         self.pending = []
         self.done = set()
+        # on_reduced(blk): called on the comm stream right after the block's buckets are reduced (the Trainer
+        # releases that block's AdamW there, overlapping the remaining backward and all-reduces)
+        self.on_reduced = None
 
     def broadcast_params(self, fp):
         dist.broadcast(fp.data, src=0, group=self.group)
@@ -138,6 +143,8 @@ class GradAllReducer(object):
                     t1 = torch.cuda.Event(enable_timing=True)
                     t1.record()
                     self.cur.append((t0, t1))
+            if self.on_reduced is not None:
+                self.on_reduced(blk)
 
     def grad_ready(self, kind, index):
         if kind in ("t", "v", "c"):

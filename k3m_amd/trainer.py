@@ -142,8 +142,8 @@ def block_runs(fp, weight_decay=0.01, lr_mult=None, frozen_names=()):
 
 
 # AdamW of each gradient block on a side stream as soon as the backward has finished that block (single
-# process, no gradient accumulation pending): the HBM-bound sweep overlaps the rest of the backward instead of
-# following it.  K3M_OPT_OVERLAP=0 restores the one sweep after the backward.
+# process) or the block's gradient buckets are all-reduced (DDP), on the last micro-step: the HBM-bound sweep
+# overlaps the rest of the backward instead of following it.  K3M_OPT_OVERLAP=0 restores the one sweep.
 OPT_OVERLAP = os.environ.get("K3M_OPT_OVERLAP", "1") != "0"
 # Replay a repeated step as one hipGraph (k3m_amd/graph.py): "auto" (default) when the eager step's host issue
 # time is a large share of its GPU time, "1" always, "0" never (every launch issued from Python).
@@ -286,15 +286,18 @@ class Trainer(object):
             if n:
                 self._adamw(off, n, wd, mult, step, grad_scale, flags)
 
-    def _overlap_begin(self):
+    def _overlap_begin(self, grad_scale=1.0):
         """State of an overlapped optimizer step: blocks still to update and the side stream."""
         dev = self.engine.fp.device
         if self.opt_stream is None:
             self.opt_stream = torch.cuda.Stream(device=dev)
         self._pending = set(self.block_runs)
         self._flags = L.ADAM_ZERO_GRAD | (L.ADAM_APEX if self.optimizer == "fused_adam" else 0)
+        self._grad_scale = grad_scale
 
     def _overlap_block(self, blk):
+        """The block's AdamW on the side stream, after everything issued so far on the CURRENT stream (the
+        compute stream at a backward hand-off; the comm stream after the block's all-reduce under DDP)."""
         if blk not in self._pending:
             return
         self._pending.discard(blk)
@@ -302,7 +305,7 @@ class Trainer(object):
         ev.record()
         with torch.cuda.stream(self.opt_stream):
             self.opt_stream.wait_event(ev)
-            self._adam_runs(self.block_runs[blk], self.global_step + 1, 1.0, self._flags)
+            self._adam_runs(self.block_runs[blk], self.global_step + 1, self._grad_scale, self._flags)
 
     def _overlap_hook(self, kind, index):
         # the heads / fusion / structure gradients are final before the first encoder block's (ddp.grad_ready)
@@ -414,11 +417,15 @@ class Trainer(object):
             out["masked_img_loss"] * self.loss_img_weight
         last = self.micro + 1 == self.accum_steps
         sync = self.ddp is not None and last
-        overlap = (self.overlap and last and self.ddp is None and self.ADAMW is None and fp_is_cuda(eng))
+        overlap = self.overlap and last and self.ADAMW is None and fp_is_cuda(eng)
         hook = None
         if sync:
             self.ddp.begin(eng)
             hook = self.ddp.grad_ready
+            if overlap:   # each block's AdamW (1/world folded in) as soon as its buckets are reduced
+                eng.check_hints()
+                self._overlap_begin(grad_scale=1.0 / self.ddp.world)
+                self.ddp.on_reduced = self._overlap_block
         elif overlap:
             eng.check_hints()   # a completed label-count check that failed raises before any update
             self._overlap_begin()
@@ -429,6 +436,9 @@ class Trainer(object):
         self.micro += 1
         if last:
             if overlap:
+                if sync:
+                    self.ddp.finish()
+                    self.ddp.on_reduced = None
                 self._overlap_finish()
             else:
                 eng.check_hints()   # a completed label-count check that failed raises before the update

@@ -29,6 +29,13 @@ SHAPES = [
     ("co pv ffn1", "nt", 8192, 3072, 768, L.EPI_BIAS_GELU),
     ("co txt dgrad", "nn", 2304, 768, 3072, L.EPI_NONE),
     ("co img wgrad", "tn", 1024, 1024, 2368, L.EPI_NONE),
+    # image-layer (4,736 rows) and small head shapes of the step (scripts/gemm_calls.py)
+    ("img dgrad dgelu", "nn", 4736, 1024, 1024, L.EPI_DGELU),
+    ("img dgrad plain", "nn", 4736, 1024, 1024, L.EPI_NONE),
+    ("img fwd gelu", "nt", 4736, 1024, 1024, L.EPI_BIAS_GELU),
+    ("img fwd bias", "nt", 4736, 1024, 1024, L.EPI_BIAS),
+    ("loc wgrad", "tn", 1024, 5, 2368, L.EPI_NONE),
+    ("mlm wgrad", "tn", 768, 768, 1552, L.EPI_NONE),
     # square reference shapes (the CDNA guide quotes its bf16 templates at 4096^3)
     ("sq4k nt", "nt", 4096, 4096, 4096, L.EPI_NONE),
     ("sq4k ffn1-k", "nt", 20992, 3072, 4096, L.EPI_NONE),
