@@ -109,8 +109,30 @@ class BertForMultiModalPreTraining_tri_stru(nn.Module):
         pass  # the decoder IS the word-embedding view of the flat buffer
 
     def half(self):
-        raise NotImplementedError("fp16 model weights are not supported; the MI355X path keeps fp32 master "
-                                  "weights (mixed-precision GEMMs are selected by the engine)")
+        """``model.half()`` of the --fp16 / --apex_fast branch (train_concap_struc.py:299-300, before the optimizer
+        is built at :352-441).  The reference casts the weights to fp16 and apex keeps fp32 master copies; here the
+        engine switches to its 16-bit mode (bf16 encoder GEMMs and attention — the MI355X 16-bit matrix format —
+        fp32 master weights, heads and optimizer).  Parameter names, order and values are kept; the parameters
+        become views of the new engine's buffer, so build the optimizer after this call, as the driver does.
+        The driver's ``.half()`` inputs (:496-499) are accepted: forward reads them as fp32."""
+        if self.engine.dtype == "bf16":
+            return self
+        old = self.engine
+        eng = K3MEngine(self.config, old.device, seed=old.base_seed, dtype="bf16")
+        with torch.no_grad():
+            eng.fp.data.copy_(old.fp.data)
+            eng.fp.grad.copy_(old.fp.grad)
+        eng.fp.shadow_fresh = False
+        eng.step_count = old.step_count
+        self.engine = eng
+        for n in self._names:
+            key = n.replace(".", "__")
+            grad = getattr(self, key).grad
+            p = nn.Parameter(eng.fp.p[n], requires_grad=True)
+            self._parameters[key] = p
+            if grad is not None:
+                p.grad = eng.fp.g[n]
+        return self
 
     # --- gradients live in the engine's flat buffer
     def _prepare_grads(self):

@@ -209,3 +209,37 @@ def test_standin_adamw_state_layout_roundtrip(dev):
     bad.grad = torch.ones_like(bad)
     with pytest.raises(ValueError, match="moments"):
         opt3.step()
+
+
+def test_half_switches_to_bf16_mode(dev):
+    """``model.half()`` (train_concap_struc.py:299-300): same 998 parameters with the same values, now views of
+    the 16-bit engine's buffer (bf16 encoder, fp32 master weights); the driver's fp16 inputs (:496-499) are
+    accepted; forward / backward run and the losses stay within the bf16 mode's bars of the fp32 model's."""
+    from vilbert_k3m.vilbert_k3m import BertForMultiModalPreTraining_tri_stru
+    from k3m_amd.weights import param_values
+    g = load_case("bs2_hard")
+    cfg = case_config(g)
+    model = BertForMultiModalPreTraining_tri_stru(cfg, device=dev)
+    vals = param_values(cfg, int(g["weight_seed"]))
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()})
+    model.eval()
+    tb = {k: v.to(dev) for k, v in case_batch(g).items()}
+    noise = {k: v.to(dev) for k, v in case_noise(g).items()}
+    ent, val = torch.from_numpy(g["ent_neg"]), torch.from_numpy(g["val_neg"])
+    ref = [float(x) for x in _driver_forward(model, tb, dev, noise, ent, val)[:2]]
+    before = {n: p.detach().clone() for n, p in model.named_parameters()}
+    assert model.half() is model and model.engine.dtype == "bf16"
+    named = list(model.named_parameters())
+    assert [n for n, _ in named] == list(before)
+    for n, p in named:
+        assert p.dtype == torch.float32 and torch.equal(p.detach(), before[n]), n
+        assert p.data_ptr() == model.engine.fp.p[n].data_ptr()
+    for k in ("image_feat", "image_loc", "image_target"):
+        tb[k] = tb[k].half()
+    outs = _driver_forward(model, tb, dev, noise, ent, val)
+    got = [float(x) for x in outs[:2]]
+    np.testing.assert_allclose(got, ref, rtol=3e-2, atol=1e-3)
+    loss = outs[0] + outs[1] + outs[3] + outs[9]
+    loss.backward()
+    gq = dict(model.named_parameters())["encoder.layer.0.attention.self.query.weight"].grad
+    assert gq is not None and torch.isfinite(gq).all() and float(gq.abs().max()) > 0
