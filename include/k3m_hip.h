@@ -191,6 +191,11 @@ int k3m_ce_fwd_bwd(float* logits, long long ld, const int64_t* labels, const flo
  * sum_c xlogy(t,t) - t*logsoftmax(pred); pred overwritten by scale*(softmax*sum(t) - t). */
 int k3m_kl_fwd_bwd(float* logits, long long ld, const float* target, long long ldt, const int32_t* trow,
                    const float* row_scale, int rows, int ncls, float* loss_rows, hipStream_t stream);
+/* x[r][c] *= (slot[r] == 0 ? w0 : w1): the shared MLM decoder's gradient rows of the text (slot 0) and PV
+ * (slot 1) heads weighted by their losses' upstream gradients (a caller's w_t*mlm_t + w_pv*mlm_pv; the
+ * reference sums them with weight 1, train_concap_struc.py:531-533). */
+int k3m_scale_rows_by_slot(float* x, long long ld, const int32_t* slot, int rows, int cols, float w0, float w1,
+                           hipStream_t stream);
 /* out[slot[r]] += loss_rows[r] * row_scale[r] for slots 0..3 (single block). */
 int k3m_loss_reduce(const float* loss_rows, const float* row_scale, const int32_t* slot, int rows, float* out,
                     hipStream_t stream);

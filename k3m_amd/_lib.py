@@ -59,6 +59,7 @@ SIGNATURES = {
     "k3m_ce_fwd_bwd": [vp, i64, vp, vp, i32, i32, vp, vp],
     "k3m_kl_fwd_bwd": [vp, i64, vp, i64, vp, vp, i32, i32, vp, vp],
     "k3m_loss_reduce": [vp, vp, vp, i32, vp, vp],
+    "k3m_scale_rows_by_slot": [vp, i64, vp, i32, i32, f32, f32, vp],
     "k3m_nsp_loss": [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp],
     "k3m_relu_cat3": [vp, vp, vp, vp, i32, i32, i32, vp],
     "k3m_gate_fwd": [vp, vp, vp, vp, vp, vp, i32, i32, u64, u64, i32, vp],

@@ -111,6 +111,17 @@ __global__ __launch_bounds__(256) void kl_kernel(float* __restrict__ logits, lon
   }
 }
 
+// gradient rows of the text / PV MLM heads (slot 0 / 1 of the shared decoder's labelled rows) weighted by their
+// losses' upstream gradients, which differ only when a caller weights mlm_t and mlm_pv differently
+__global__ __launch_bounds__(256) void scale_rows_slot_kernel(float* __restrict__ x, long long ld,
+                                                              const int32_t* __restrict__ slot, int cols, float w0,
+                                                              float w1) {
+  const int r = blockIdx.x;
+  const float w = slot[r] == 0 ? w0 : w1;
+  float* row = x + (long long)r * ld;
+  for (int c = threadIdx.x; c < cols; c += 256) row[c] *= w;
+}
+
 __global__ __launch_bounds__(256) void loss_reduce_kernel(const float* __restrict__ lr, const float* __restrict__ sc,
                                                           const int32_t* __restrict__ slot, int rows,
                                                           float* __restrict__ out) {
@@ -182,6 +193,15 @@ extern "C" int k3m_kl_fwd_bwd(float* logits, long long ld, const float* target, 
   if (rows == 0) return 0;
   hipLaunchKernelGGL(kl_kernel, dim3(rows), dim3(256), 0, st, logits, ld, target, ldt, trow, row_scale, ncls,
                      loss_rows);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_scale_rows_by_slot(float* x, long long ld, const int32_t* slot, int rows, int cols, float w0,
+                                      float w1, hipStream_t st) {
+  if (rows == 0) return 0;
+  K3M_ARG(x && slot && rows > 0 && cols > 0 && ld >= cols);
+  hipLaunchKernelGGL(scale_rows_slot_kernel, dim3(rows), dim3(256), 0, st, x, ld, slot, cols, w0, w1);
   K3M_CHECK_LAUNCH();
   return 0;
 }

@@ -902,6 +902,7 @@ class K3MEngine(object):
             L.call("k3m_loss_reduce", lr_m.data_ptr(), sc_m.data_ptr(), sl_m.data_ptr(), n_m, losses.data_ptr(),
                    L.stream())
         ctx["mlm"] = (idx_m, n_m, hm, pre_m, hl, xh_m, rs_m, logits)
+        ctx["mlm_slot"] = sl_m   # 0: text row, 1: PV row (k3m_scale_rows_by_slot)
 
         Cv = c.v_target_size
         hv = torch.empty((n_v, Hv), dtype=torch.float32, device=dev)
@@ -944,8 +945,9 @@ class K3MEngine(object):
         return out, ctx
 
     # ------------------------------------------------------------ backward
-    def backward(self, ctx, w_mlm=1.0, w_img=1.0, w_lpm=1.0, grad_ready=None):
-        """Backward of  w_mlm*(mlm_t + mlm_pv) + w_img*img + w_lpm*lpm  (train_concap_struc.py:533).
+    def backward(self, ctx, w_mlm=1.0, w_img=1.0, w_lpm=1.0, grad_ready=None, w_mlm_pv=None):
+        """Backward of  w_mlm*(mlm_t + mlm_pv) + w_img*img + w_lpm*lpm  (train_concap_struc.py:533); with
+        w_mlm_pv given, of  w_mlm*mlm_t + w_mlm_pv*mlm_pv + ...  (a caller weighting the two MLM losses apart).
         Parameter gradients are ACCUMULATED into self.fp.grad.  grad_ready(kind, index) is called as
         soon as the gradients of an encoder block are final (DDP bucket hook).
 
@@ -958,9 +960,9 @@ class K3MEngine(object):
                 dr.flush()
                 if grad_ready is not None:
                     grad_ready(kind, index)
-            self._backward(ctx, w_mlm, w_img, w_lpm, hook)
+            self._backward(ctx, w_mlm, w_img, w_lpm, hook, w_mlm_pv)
 
-    def _backward(self, ctx, w_mlm=1.0, w_img=1.0, w_lpm=1.0, grad_ready=None):
+    def _backward(self, ctx, w_mlm=1.0, w_img=1.0, w_lpm=1.0, grad_ready=None, w_mlm_pv=None):
         c = self.cfg
         fp = self.fp
         dev = self.device
@@ -974,6 +976,11 @@ class K3MEngine(object):
 
         # ---- MLM head (dlogits already in place from the forward CE kernel)
         idx_m, n_m, hm, pre_m, hl, xh_m, rs_m, dlog = ctx["mlm"] if "mlm" in ctx else (None, 0) + (None,) * 6
+        if n_m and w_mlm_pv is not None and w_mlm_pv != w_mlm:
+            # text and PV rows of the shared decoder carry different upstream weights: fold them into the rows
+            L.call("k3m_scale_rows_by_slot", dlog.data_ptr(), dlog.shape[1], ctx["mlm_slot"].data_ptr(), n_m,
+                   dlog.shape[1], w_mlm, w_mlm_pv, L.stream())
+            w_mlm = 1.0
         if n_m:
             bf = self.dtype == "bf16"
             E = fp.p16("embeddings.word_embeddings.weight") if bf else fp.p["embeddings.word_embeddings.weight"]

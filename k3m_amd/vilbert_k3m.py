@@ -37,14 +37,12 @@ class _Step(torch.autograd.Function):
         def val(g):
             return 0.0 if g is None else float(g.reshape(-1)[0])
         wt, wpv = val(g_t), val(g_pv)
-        if wt != wpv:
-            raise NotImplementedError("different upstream weights for the text and PV MLM losses")
         if g_ci is not None:
             ectx["d_c_initial"] = g_ci
         if g_cf is not None:
             ectx["d_c_final"] = g_cf
         model._prepare_grads()
-        model.engine.backward(ectx, w_mlm=wt, w_img=val(g_img), w_lpm=val(g_lpm))
+        model.engine.backward(ectx, w_mlm=wt, w_img=val(g_img), w_lpm=val(g_lpm), w_mlm_pv=wpv)
         model._expose_grads()
         fctx.ectx = None
         return None, None, None, None

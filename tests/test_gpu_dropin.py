@@ -243,3 +243,37 @@ def test_half_switches_to_bf16_mode(dev):
     loss.backward()
     gq = dict(model.named_parameters())["encoder.layer.0.attention.self.query.weight"].grad
     assert gq is not None and torch.isfinite(gq).all() and float(gq.abs().max()) > 0
+
+
+def test_unequal_mlm_loss_weights(dev):
+    """A caller's  a*mlm_t + b*mlm_pv  (the reference sums them with weight 1, train_concap_struc.py:531-533): the
+    shared decoder's text and PV gradient rows take their own upstream weights (k3m_scale_rows_by_slot), so the
+    gradient equals a * grad(mlm_t) + b * grad(mlm_pv), to the backward's float-atomics rounding."""
+    from vilbert_k3m.vilbert_k3m import BertForMultiModalPreTraining_tri_stru
+    from k3m_amd.weights import param_values
+    g = load_case("bs2_hard")
+    cfg = case_config(g)
+    model = BertForMultiModalPreTraining_tri_stru(cfg, device=dev)
+    vals = param_values(cfg, int(g["weight_seed"]))
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()})
+    model.eval()
+    tb = {k: v.to(dev) for k, v in case_batch(g).items()}
+    noise = {k: v.to(dev) for k, v in case_noise(g).items()}
+    ent, val = torch.from_numpy(g["ent_neg"]), torch.from_numpy(g["val_neg"])
+    names = ("cls.predictions.bias", "cls.predictions.transform.dense.weight", "embeddings.word_embeddings.weight",
+             "encoder.layer.11.output.dense.weight", "encoder.layer.0.attention.self.query.weight")
+
+    def grads(wt, wpv):
+        model.zero_grad(set_to_none=True)
+        outs = _driver_forward(model, tb, dev, noise, ent, val)
+        (wt * outs[0] + wpv * outs[3]).backward()
+        named = dict(model.named_parameters())
+        return {n: named[n].grad.detach().double().clone() for n in names}
+    a, b = 0.7, 1.3
+    both = grads(a, b)
+    gt = grads(1.0, 0.0)
+    gp = grads(0.0, 1.0)
+    for n in names:
+        ref = a * gt[n] + b * gp[n]
+        err = float((both[n] - ref).norm())
+        assert err <= 1e-5 * float(ref.norm()) + 1e-9, (n, err, float(ref.norm()))
