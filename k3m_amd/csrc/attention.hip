@@ -1211,6 +1211,305 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_reg_kernel(
   ATT_STAMP_END(4);
 }
 
+// ------------------------------------------------------------------ backward on the bf16 matrix cores, keys on lanes
+// fp32 backward with every product in the bf16x6 form (gemm_x6_tile.h; the forward's attn_fwd_x6_kernel), laid out
+// like attention_bf16.hip's key-major kernel:
+//   staging     Q, dO and K split exactly into three bf16 planes each, stored as [rows][HD] bf16 images (16-B chunk
+//               c of row r at c ^ swz(r)), so row fragments (ds_read_b128) and transposed fragments
+//               (ds_read_b64_tr_b16) of every plane are conflict-free; D = rowsum(dO o O) from fp32 chunk dots;
+//   key phase   wave w owns keys 32w..32w+31 on the MFMA lanes (its V rows split into B fragments in registers);
+//               per 32-query tile dPd = dO V^T, then with P from the forward's probabilities and m the regenerated
+//               dropout scale: Pd = P m, dS = P (dPd m - D) in the accumulators; dV^T += dO^T Pd and
+//               dK^T += Q^T dS take Pd / dS split straight from the accumulators (accumulator k order) as B operands,
+//               A = transposed plane reads; dS is kept in fp32 registers;
+//   dS^T        three planes written once over the Q / dO images;
+//   query phase dQ = scale dS K (A = dS^T planes, B = K planes, both transposed reads).
+// ML: rows staged (>= LQ, LK), NW = ML / 32 waves.  Same semantics and dropout counters as attn_bwd_reg_kernel.
+typedef short k6short4 __attribute__((ext_vector_type(4)));
+typedef short k6short8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) k6short4 k6lds_short4;
+
+template <int NC>
+__device__ __forceinline__ int k6_ioff(int r, int c) {   // element offset of 8-bf16 chunk c of row r
+  if constexpr (NC == 16) return r * 128 + ((c ^ (((r & 3) << 2) | ((r >> 2) & 3))) << 3);
+  else if constexpr (NC == 8) return r * 64 + ((c ^ ((((r >> 1) & 1) << 2) | ((r >> 2) & 3))) << 3);
+  else return r * 32 + (c << 3);
+}
+__device__ __forceinline__ int k6_ioff_n(int nc, int r, int c) {
+  return nc == 4 ? k6_ioff<4>(r, c) : nc == 8 ? k6_ioff<8>(r, c) : k6_ioff<16>(r, c);
+}
+// row fragment: X[rbase + (lane&31)][16 ks + 8 (lane>>5) .. +7]
+template <int NC>
+__device__ __forceinline__ x6bf16x8 k6_row(const uint16_t* img, int rbase, int ks, int lane) {
+  return *reinterpret_cast<const x6bf16x8*>(img + k6_ioff<NC>(rbase + (lane & 31), 2 * ks + (lane >> 5)));
+}
+// transposed fragment (attention_bf16.hip trfrag): element e of lane l = X[row(e)][cbase + (l&31)],
+// PERM = false: row(e) = rbase + 8h + e; PERM = true: row(e) = rbase + 8(e>>2) + 4h + (e&3)
+template <int NC, bool PERM>
+__device__ __forceinline__ x6bf16x8 k6_tr(const uint16_t* img, int rbase, int cbase, int lane) {
+  const int g = lane >> 4, qq = (lane >> 2) & 3, p = lane & 3, h = lane >> 5;
+  const int ch = ((cbase + 16 * (g & 1)) >> 3) + (p >> 1);
+  const int r0 = PERM ? rbase + 4 * h + qq : rbase + 8 * h + qq;
+  const int r1 = PERM ? r0 + 8 : r0 + 4;
+  const k6short4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((k6lds_short4*)(img + k6_ioff<NC>(r0, ch) + 4 * (p & 1)));
+  const k6short4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((k6lds_short4*)(img + k6_ioff<NC>(r1, ch) + 4 * (p & 1)));
+  const k6short8 vv = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+  return __builtin_bit_cast(x6bf16x8, vv);
+}
+__device__ __forceinline__ x6bf16x8 k6_tr_n(const uint16_t* img, int nc, int rbase, int cbase, int lane) {
+  if (nc == 4) return k6_tr<4, false>(img, rbase, cbase, lane);
+  if (nc == 8) return k6_tr<8, false>(img, rbase, cbase, lane);
+  return k6_tr<16, false>(img, rbase, cbase, lane);
+}
+// x = h + m + l exactly for 4 floats -> three packed bf16 quads
+__device__ __forceinline__ void k6_split4(const float4 v, uint2& hq, uint2& mq, uint2& lq) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+  uint32_t H[2], Mm[2], Lw[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const float a = x[2 * p], b = x[2 * p + 1];
+    const uint32_t hh = x6_pk(a, b);
+    const float r1a = a - __uint_as_float(hh << 16), r1b = b - __uint_as_float(hh & 0xffff0000u);
+    const uint32_t mm = x6_pk(r1a, r1b);
+    const float r2a = r1a - __uint_as_float(mm << 16), r2b = r1b - __uint_as_float(mm & 0xffff0000u);
+    H[p] = hh;
+    Mm[p] = mm;
+    Lw[p] = x6_pk(r2a, r2b);
+  }
+  hq = make_uint2(H[0], H[1]);
+  mq = make_uint2(Mm[0], Mm[1]);
+  lq = make_uint2(Lw[0], Lw[1]);
+}
+// accumulator registers 8s..8s+7 split into three bf16 operand fragments
+__device__ __forceinline__ void k6_accsplit(const floatx16& a, int s, x6bf16x8& h, x6bf16x8& m, x6bf16x8& l) {
+  float t[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = a[8 * s + e];
+  x6_split8(t, h, m, l);
+}
+
+template <int HD, int ML>
+__global__ __launch_bounds__(ML * 2, 1) void attn_bwd_x6km_kernel(
+    const float* __restrict__ dctx, long long ldc, const float* __restrict__ o, long long ldo,
+    const float* __restrict__ q, long long ldq, const float* __restrict__ k, long long ldk,
+    const float* __restrict__ v, long long ldv, const float* __restrict__ probs, float* __restrict__ dq,
+    float* __restrict__ dk, float* __restrict__ dv, long long lddq, long long lddk, long long lddv, int lq, int lk,
+    int nh, float scale, float p_drop, uint64_t seed, uint64_t off) {
+  constexpr int NW = ML / 32, NTH = NW * 64;
+  constexpr int NC = HD / 8, HW = HD, KS = HD / 16, DT = HD / 32, NCH = HD / 4;
+  extern __shared__ float smem_f[];   // (the file's other kernels declare the dynamic LDS as float[])
+  uint16_t* smem = reinterpret_cast<uint16_t*>(smem_f);
+  const int s = blockIdx.x / nh, h = blockIdx.x % nh;
+  const int LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
+  const int QW = LQ == 96 ? 128 : LQ, QNC = QW / 8;   // dS^T image [LK][QW] per plane
+  const int PQ = LQ * HW, PK = LK * HW, PS = LK * QW;   // bf16 elements per plane
+  const int RQ = max(6 * PQ, 3 * PS);                  // Q | dO planes, later the dS^T planes
+  uint16_t* Qs = smem;
+  uint16_t* dOs = smem + 3 * PQ;
+  uint16_t* dSt = smem;
+  uint16_t* Ks = smem + RQ;
+  float* Ds = reinterpret_cast<float*>(Ks + 3 * PK);
+  float* scr = Ds + LQ;   // [LQ][NCH] chunk dots of dO and O
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
+  const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
+  const int hoff = h * HD;
+  const long long pbase = ((long long)s * nh + h) * lq * lk;
+  const K3mDrop dr = k3m_drop_init(seed, p_drop);
+  const int NQT = LQ >> 5;
+  const int j = 32 * w + cl;     // this lane's key in the key phase
+  const bool kw = 32 * w < LK;   // wave-uniform
+
+  // this wave's V rows split into B-operand fragments (lane -> key j, dims 16 ks + 8 kl .. +7)
+  x6bf16x8 vh[KS], vm[KS], vl[KS];
+  {
+    const bool okv = kw && j < lk;
+    const float* vp = v + (krow0 + min(j, lk - 1)) * ldv + hoff + 8 * kl;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const float4 a = keep4(okv, *reinterpret_cast<const float4*>(vp + 16 * ks));
+      const float4 b = keep4(okv, *reinterpret_cast<const float4*>(vp + 16 * ks + 4));
+      const float t[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      x6_split8(t, vh[ks], vm[ks], vl[ks]);
+    }
+  }
+  {
+    // staging: every global load (Q, dO, O, K float4 chunks) issued before the first LDS write
+    constexpr int U = ML * NCH / NTH;
+    float4 rq[U], rdo[U], ro[U], rk[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = threadIdx.x + u * NTH, i = e / NCH, c = e % NCH;
+      const long long qo = qrow0 + min(i, lq - 1), ko = krow0 + min(i, lk - 1);
+      rq[u] = keep4(i < lq, *reinterpret_cast<const float4*>(q + qo * ldq + hoff + 4 * c));
+      rdo[u] = keep4(i < lq, *reinterpret_cast<const float4*>(dctx + qo * ldc + hoff + 4 * c));
+      ro[u] = keep4(i < lq, *reinterpret_cast<const float4*>(o + qo * ldo + hoff + 4 * c));
+      rk[u] = keep4(i < lk, *reinterpret_cast<const float4*>(k + ko * ldk + hoff + 4 * c));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = threadIdx.x + u * NTH, i = e / NCH, c = e % NCH;
+      const int eo = 4 * (c & 1);
+      if (i < LQ) {
+        const int io = k6_ioff<NC>(i, c >> 1) + eo;
+        uint2 a, b, cc;
+        k6_split4(rq[u], a, b, cc);
+        *reinterpret_cast<uint2*>(Qs + io) = a;
+        *reinterpret_cast<uint2*>(Qs + PQ + io) = b;
+        *reinterpret_cast<uint2*>(Qs + 2 * PQ + io) = cc;
+        k6_split4(rdo[u], a, b, cc);
+        *reinterpret_cast<uint2*>(dOs + io) = a;
+        *reinterpret_cast<uint2*>(dOs + PQ + io) = b;
+        *reinterpret_cast<uint2*>(dOs + 2 * PQ + io) = cc;
+        scr[e] = rdo[u].x * ro[u].x + rdo[u].y * ro[u].y + rdo[u].z * ro[u].z + rdo[u].w * ro[u].w;
+      }
+      if (i < LK) {
+        const int io = k6_ioff<NC>(i, c >> 1) + eo;
+        uint2 a, b, cc;
+        k6_split4(rk[u], a, b, cc);
+        *reinterpret_cast<uint2*>(Ks + io) = a;
+        *reinterpret_cast<uint2*>(Ks + PK + io) = b;
+        *reinterpret_cast<uint2*>(Ks + 2 * PK + io) = cc;
+      }
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < LQ) {
+      float acc = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) acc += scr[threadIdx.x * NCH + c];
+      Ds[threadIdx.x] = acc;
+    }
+  }
+  __syncthreads();
+
+  floatx16 dsv[ML / 32];   // dS of each query tile (fp32; rows: queries 32 it + crow, lane: key j)
+  if (kw) {
+    floatx16 dV[DT], dK[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        dV[dt][r] = 0.f;
+        dK[dt][r] = 0.f;
+      }
+    const int jc = min(j, lk - 1);
+    const bool jok = j < lk;
+#pragma unroll
+    for (int it = 0; it < ML / 32; ++it) {
+      if (it >= NQT) break;
+      // the forward's probabilities of this tile, issued ahead of the dP MFMAs (unconditional, clamped)
+      float p[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = 32 * it + (r & 3) + 8 * (r >> 2) + 4 * kl;
+        const float pv = probs[pbase + (long long)min(i, lq - 1) * lk + jc];
+        p[r] = (i < lq && jok) ? pv : 0.f;
+      }
+      floatx16 dP;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dP[r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        x6_mma(dP, k6_row<NC>(dOs, 32 * it, ks, lane), k6_row<NC>(dOs + PQ, 32 * it, ks, lane),
+               k6_row<NC>(dOs + 2 * PQ, 32 * it, ks, lane), vh[ks], vm[ks], vl[ks]);
+      floatx16 Pd;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int i0 = 32 * it + 8 * a + 4 * kl;
+        const float4 d4 = *reinterpret_cast<const float4*>(Ds + i0);
+        const float dd[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int r = 4 * a + b, i = i0 + b;
+          const float m = k3m_drop(dr, off + pbase + (long long)min(i, lq - 1) * lk + jc);
+          Pd[r] = p[r] * m;
+          dP[r] = p[r] * (dP[r] * m - dd[b]);   // dS
+        }
+      }
+      dsv[it] = dP;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        x6bf16x8 ph, pm, pl, sh, sm, sl;
+        k6_accsplit(Pd, s2, ph, pm, pl);
+        k6_accsplit(dP, s2, sh, sm, sl);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const int rb = 32 * it + 16 * s2, cb = 32 * dt;
+          x6_mma(dV[dt], k6_tr<NC, true>(dOs, rb, cb, lane), k6_tr<NC, true>(dOs + PQ, rb, cb, lane),
+                 k6_tr<NC, true>(dOs + 2 * PQ, rb, cb, lane), ph, pm, pl);
+          x6_mma(dK[dt], k6_tr<NC, true>(Qs, rb, cb, lane), k6_tr<NC, true>(Qs + PQ, rb, cb, lane),
+                 k6_tr<NC, true>(Qs + 2 * PQ, rb, cb, lane), sh, sm, sl);
+        }
+      }
+    }
+    // dV^T / dK^T: lane -> key j, register r -> d = 32 dt + 8 (r >> 2) + 4 kl + (r & 3): 16-B stores
+    if (jok) {
+      float* pv = dv + (krow0 + j) * lddv + hoff + 4 * kl;
+      float* pk = dk + (krow0 + j) * lddk + hoff + 4 * kl;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          *reinterpret_cast<float4*>(pv + 32 * dt + 8 * a) =
+              make_float4(dV[dt][4 * a], dV[dt][4 * a + 1], dV[dt][4 * a + 2], dV[dt][4 * a + 3]);
+          *reinterpret_cast<float4*>(pk + 32 * dt + 8 * a) =
+              make_float4(dK[dt][4 * a] * scale, dK[dt][4 * a + 1] * scale, dK[dt][4 * a + 2] * scale,
+                          dK[dt][4 * a + 3] * scale);
+        }
+    }
+  }
+  __syncthreads();   // every wave is past its last read of Q / dO
+  if (kw) {
+    // dS^T[j][i] planes: registers 4a..4a+3 of tile it are queries 32 it + 8 a + 4 kl .. +3 (8 bytes per plane)
+#pragma unroll
+    for (int it = 0; it < ML / 32; ++it) {
+      if (it >= NQT) break;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        uint2 x, y, z;
+        k6_split4(make_float4(dsv[it][4 * a], dsv[it][4 * a + 1], dsv[it][4 * a + 2], dsv[it][4 * a + 3]), x, y, z);
+        const int io = k6_ioff_n(QNC, j, 4 * it + a) + 4 * kl;
+        *reinterpret_cast<uint2*>(dSt + io) = x;
+        *reinterpret_cast<uint2*>(dSt + PS + io) = y;
+        *reinterpret_cast<uint2*>(dSt + 2 * PS + io) = z;
+      }
+    }
+  }
+  __syncthreads();
+  // query phase: dQ = scale dS K, tile it of 32 queries per wave (lane -> d, registers -> queries)
+  for (int it = w; it < NQT; it += NW) {
+    floatx16 oq[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oq[dt][r] = 0.f;
+    for (int kk = 0; kk < LK / 16; ++kk) {
+      const x6bf16x8 ah = k6_tr_n(dSt, QNC, 16 * kk, 32 * it, lane);
+      const x6bf16x8 am = k6_tr_n(dSt + PS, QNC, 16 * kk, 32 * it, lane);
+      const x6bf16x8 al = k6_tr_n(dSt + 2 * PS, QNC, 16 * kk, 32 * it, lane);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+        x6_mma(oq[dt], ah, am, al, k6_tr<NC, false>(Ks, 16 * kk, 32 * dt, lane),
+               k6_tr<NC, false>(Ks + PK, 16 * kk, 32 * dt, lane), k6_tr<NC, false>(Ks + 2 * PK, 16 * kk, 32 * dt, lane));
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ii = 32 * it + (r & 3) + 8 * (r >> 2) + 4 * kl;
+      if (ii < lq) {
+        float* dst = dq + (qrow0 + ii) * lddq + hoff + cl;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) dst[32 * dt] = oq[dt][r] * scale;
+      }
+    }
+  }
+}
+
+size_t bwd_x6km_lds(int lq, int lk, int hd) {
+  const size_t LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
+  const size_t QW = LQ == 96 ? 128 : LQ;
+  return 2 * (std::max(6 * LQ * hd, 3 * LK * QW) + 3 * LK * hd) + 4 * (LQ + LQ * (hd / 4));
+}
+
 size_t bwd_reg_lds(int lq, int lk, int hd) {
   const size_t LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
   return sizeof(float) * (2 * LQ * hd + LK * hd + LQ + LQ * (hd / 4));
@@ -1328,6 +1627,25 @@ extern "C" int k3m_attn_fwd(const void* q, long long ldq, const void* k, long lo
 }
 
 static const bool kAttnBwdReg = k3m_env_flag("K3M_ATTN_BWD_REG", true);
+// the fp32 backward's products on the bf16 matrix cores (attn_bwd_x6km_kernel, d = 64); K3M_ATTN_BWD_X6=0 keeps
+// the f32-MFMA kernels
+static const bool kAttnBwdX6 = k3m_env_flag("K3M_ATTN_BWD_X6", false);
+
+template <int ML>
+void launch_bwd_x6km(const void* dctx, long long ldc, const void* o, long long ldo, const void* q, long long ldq,
+                     const void* k, long long ldk, const void* v, long long ldv, const float* probs, void* dq, void* dk,
+                     void* dv, long long lddq, long long lddk, long long lddv, int nseq, int lq, int lk, int nh,
+                     float scale, float p_drop, uint64_t seed, uint64_t off, size_t lds, hipStream_t st) {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)attn_bwd_x6km_kernel<64, ML>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_MAX);
+    done = true;
+  }
+  hipLaunchKernelGGL((attn_bwd_x6km_kernel<64, ML>), dim3(nseq * nh), dim3(ML * 2), lds, st, (const float*)dctx, ldc,
+                     (const float*)o, ldo, (const float*)q, ldq, (const float*)k, ldk, (const float*)v, ldv, probs,
+                     (float*)dq, (float*)dk, (float*)dv, lddq, lddk, lddv, lq, lk, nh, scale, p_drop, seed, off);
+}
 
 template <int HD>
 void launch_bwd_reg(const void* dctx, long long ldc, const void* o, long long ldo, const void* q, long long ldq,
@@ -1359,6 +1677,18 @@ extern "C" int k3m_attn_bwd(const void* dctx, long long ldc, const void* o, long
   K3M_ARG(lds <= (size_t)LDS_MAX);
   const bool small = lq <= 64 && lk <= 64 && hd <= 64;   // d = 128 runs better as one 8-wave block
   const int LQ = (lq + 31) & ~31;
+  if (dtype == K3M_F32 && kAttnBwdX6 && hd == 64 && bwd_x6km_lds(lq, lk, hd) <= (size_t)LDS_MAX &&
+      vec_ok(o, ldo, dtype) && vec_ok(dk, lddk, dtype) && vec_ok(dv, lddv, dtype)) {
+    const size_t xl = bwd_x6km_lds(lq, lk, hd);
+    if (small)
+      launch_bwd_x6km<64>(dctx, ldc, o, ldo, q, ldq, k, ldk, v, ldv, probs, dq, dk, dv, lddq, lddk, lddv, nseq, lq, lk,
+                          nh, scale, p_drop, seed, off, xl, st);
+    else
+      launch_bwd_x6km<128>(dctx, ldc, o, ldo, q, ldq, k, ldk, v, ldv, probs, dq, dk, dv, lddq, lddk, lddv, nseq, lq, lk,
+                           nh, scale, p_drop, seed, off, xl, st);
+    K3M_CHECK_LAUNCH();
+    return 0;
+  }
   // (for LK <= 64 the 64-row LDS kernel is faster: three workgroups per CU against one)
   if (dtype == K3M_F32 && kAttnBwdReg && (hd == 64 || hd == 96 || hd == 128) && LQ * hd <= 8192 && lk > 64 &&
       bwd_reg_lds(lq, lk, hd) <= (size_t)LDS_MAX && vec_ok(o, ldo, dtype) && vec_ok(dk, lddk, dtype) &&
