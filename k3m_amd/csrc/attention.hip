@@ -1627,9 +1627,10 @@ extern "C" int k3m_attn_fwd(const void* q, long long ldq, const void* k, long lo
 }
 
 static const bool kAttnBwdReg = k3m_env_flag("K3M_ATTN_BWD_REG", true);
-// the fp32 backward's products on the bf16 matrix cores (attn_bwd_x6km_kernel, d = 64); K3M_ATTN_BWD_X6=0 keeps
-// the f32-MFMA kernels
-static const bool kAttnBwdX6 = k3m_env_flag("K3M_ATTN_BWD_X6", false);
+// the fp32 backward's products on the bf16 matrix cores (attn_bwd_x6km_kernel, d = 64): L = 128 260 -> 215 us,
+// L = 36 84 -> 68 us per launch, fp32 step +0.6-0.9 % (profiles/r4b_ab_attn_bwd_x6.txt); K3M_ATTN_BWD_X6=0 keeps the
+// f32-MFMA kernels
+static const bool kAttnBwdX6 = k3m_env_flag("K3M_ATTN_BWD_X6", true);
 
 template <int ML>
 void launch_bwd_x6km(const void* dctx, long long ldc, const void* o, long long ldo, const void* q, long long ldq,
