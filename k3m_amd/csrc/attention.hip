@@ -1632,18 +1632,21 @@ static const bool kAttnBwdReg = k3m_env_flag("K3M_ATTN_BWD_REG", true);
 // f32-MFMA kernels
 static const bool kAttnBwdX6 = k3m_env_flag("K3M_ATTN_BWD_X6", true);
 
-template <int ML>
+// d = 128 heads of <= 64 queries and keys (image self-attention, text<->image co-attention) too (A/B knob)
+static const bool kAttnBwdX6D128 = k3m_env_flag("K3M_ATTN_BWD_X6_D128", false);
+
+template <int HD, int ML>
 void launch_bwd_x6km(const void* dctx, long long ldc, const void* o, long long ldo, const void* q, long long ldq,
                      const void* k, long long ldk, const void* v, long long ldv, const float* probs, void* dq, void* dk,
                      void* dv, long long lddq, long long lddk, long long lddv, int nseq, int lq, int lk, int nh,
                      float scale, float p_drop, uint64_t seed, uint64_t off, size_t lds, hipStream_t st) {
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)attn_bwd_x6km_kernel<64, ML>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)attn_bwd_x6km_kernel<HD, ML>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_MAX);
     done = true;
   }
-  hipLaunchKernelGGL((attn_bwd_x6km_kernel<64, ML>), dim3(nseq * nh), dim3(ML * 2), lds, st, (const float*)dctx, ldc,
+  hipLaunchKernelGGL((attn_bwd_x6km_kernel<HD, ML>), dim3(nseq * nh), dim3(ML * 2), lds, st, (const float*)dctx, ldc,
                      (const float*)o, ldo, (const float*)q, ldq, (const float*)k, ldk, (const float*)v, ldv, probs,
                      (float*)dq, (float*)dk, (float*)dv, lddq, lddk, lddv, lq, lk, nh, scale, p_drop, seed, off);
 }
@@ -1678,15 +1681,19 @@ extern "C" int k3m_attn_bwd(const void* dctx, long long ldc, const void* o, long
   K3M_ARG(lds <= (size_t)LDS_MAX);
   const bool small = lq <= 64 && lk <= 64 && hd <= 64;   // d = 128 runs better as one 8-wave block
   const int LQ = (lq + 31) & ~31;
-  if (dtype == K3M_F32 && kAttnBwdX6 && hd == 64 && bwd_x6km_lds(lq, lk, hd) <= (size_t)LDS_MAX &&
+  const bool x6d128 = kAttnBwdX6D128 && hd == 128 && lq <= 64 && lk <= 64;
+  if (dtype == K3M_F32 && kAttnBwdX6 && (hd == 64 || x6d128) && bwd_x6km_lds(lq, lk, hd) <= (size_t)LDS_MAX &&
       vec_ok(o, ldo, dtype) && vec_ok(dk, lddk, dtype) && vec_ok(dv, lddv, dtype)) {
     const size_t xl = bwd_x6km_lds(lq, lk, hd);
-    if (small)
-      launch_bwd_x6km<64>(dctx, ldc, o, ldo, q, ldq, k, ldk, v, ldv, probs, dq, dk, dv, lddq, lddk, lddv, nseq, lq, lk,
-                          nh, scale, p_drop, seed, off, xl, st);
+    if (hd == 128)
+      launch_bwd_x6km<128, 64>(dctx, ldc, o, ldo, q, ldq, k, ldk, v, ldv, probs, dq, dk, dv, lddq, lddk, lddv, nseq, lq,
+                               lk, nh, scale, p_drop, seed, off, xl, st);
+    else if (small)
+      launch_bwd_x6km<64, 64>(dctx, ldc, o, ldo, q, ldq, k, ldk, v, ldv, probs, dq, dk, dv, lddq, lddk, lddv, nseq, lq,
+                              lk, nh, scale, p_drop, seed, off, xl, st);
     else
-      launch_bwd_x6km<128>(dctx, ldc, o, ldo, q, ldq, k, ldk, v, ldv, probs, dq, dk, dv, lddq, lddk, lddv, nseq, lq, lk,
-                           nh, scale, p_drop, seed, off, xl, st);
+      launch_bwd_x6km<64, 128>(dctx, ldc, o, ldo, q, ldq, k, ldk, v, ldv, probs, dq, dk, dv, lddq, lddk, lddv, nseq, lq,
+                               lk, nh, scale, p_drop, seed, off, xl, st);
     K3M_CHECK_LAUNCH();
     return 0;
   }
