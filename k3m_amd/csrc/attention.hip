@@ -1633,7 +1633,7 @@ static const bool kAttnBwdReg = k3m_env_flag("K3M_ATTN_BWD_REG", true);
 static const bool kAttnBwdX6 = k3m_env_flag("K3M_ATTN_BWD_X6", true);
 
 // d = 128 heads of <= 64 queries and keys (image self-attention, text<->image co-attention) too (A/B knob)
-static const bool kAttnBwdX6D128 = k3m_env_flag("K3M_ATTN_BWD_X6_D128", false);
+static const bool kAttnBwdX6D128 = k3m_env_flag("K3M_ATTN_BWD_X6_D128", true);
 
 template <int HD, int ML>
 void launch_bwd_x6km(const void* dctx, long long ldc, const void* o, long long ldo, const void* q, long long ldq,
