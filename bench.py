@@ -355,6 +355,15 @@ def main():
     for _ in range(warm):
         tr.step(batch)
     barrier()
+    # host issue cost from an idle GPU (the timed loop's host time includes blocking on a full launch queue): two
+    # more untimed steps before the timed region (so a profile's last steps are the timed ones)
+    issue = []
+    for _ in range(2):
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        tr.step(batch)
+        issue.append(time.perf_counter() - h0)
+    barrier()
     # the GEMM / co-attention HIP-event probes bracket Python-issued launches: live in the timed region when the
     # step is issued eagerly; with graph replay (a captured launch cannot be bracketed by timing events) they
     # run in PROBE_STEPS eager steps right after it (same kernels, same shapes)
@@ -377,14 +386,6 @@ def main():
         dist.all_gather(gl, t)
         per_rank = [float(x) for x in gl]
         dt = max(per_rank)
-    # host issue cost from an idle GPU (the timed loop's host time includes blocking on a full launch queue)
-    issue = []
-    for _ in range(2):
-        torch.cuda.synchronize()
-        h0 = time.perf_counter()
-        tr.step(batch)
-        issue.append(time.perf_counter() - h0)
-    barrier()
     probe_steps = args.steps
     if graphed:
         probe_steps = PROBE_STEPS
