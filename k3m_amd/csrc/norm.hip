@@ -142,16 +142,18 @@ __global__ __launch_bounds__(256) void slab_batch_kernel(SlabJobs jobs) {
     floatx4* o = reinterpret_cast<floatx4*>(jobs.out[j] + c4);
     const floatx4 old = *o;   // issued first, used last
     floatx4 acc = *reinterpret_cast<const floatx4*>(src);
-    // slabs summed in order 0..nslab-1 (deterministic), loads issued 8 slabs ahead of the adds
-    int k = 1;
-    for (; k + 8 <= nslab; k += 8) {
+    // slabs summed in order 0..nslab-1 (deterministic), loads issued up to 8 slabs ahead of the adds; the
+    // last group is predicated (nslab is wave-uniform) rather than a one-load-at-a-time tail: split-K GEMMs
+    // leave 2..9 slabs, and a serial tail kept one 16-B load per lane in flight (~4 TB/s)
+    for (int k = 1; k < nslab; k += 8) {
       floatx4 t[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const floatx4*>(src + (long long)(k + u) * cols);
+      for (int u = 0; u < 8; ++u)
+        if (k + u < nslab) t[u] = *reinterpret_cast<const floatx4*>(src + (long long)(k + u) * cols);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc += t[u];
+      for (int u = 0; u < 8; ++u)
+        if (k + u < nslab) acc += t[u];
     }
-    for (; k < nslab; ++k) acc += *reinterpret_cast<const floatx4*>(src + (long long)k * cols);
     *o = jobs.accumulate[j] ? old + acc : acc;
     return;
   }
@@ -298,6 +300,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
 // layout as ln_fwd_kernel / ln_bwd_kernel (the row sums reduce in a different order).
 constexpr int MAXV8 = 4;   // 16-B chunks per lane: cols <= 32 * 8 * 4 = 1024
 
+__device__ __forceinline__ void unpack8bf(const uint4 u, float (&v)[8]) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[2 * q] = __uint_as_float(w[q] << 16);
+    v[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+  }
+}
+
 __device__ __forceinline__ void ld8bf(const bf16_t* p, float (&v)[8]) {
   const uint4 u = *reinterpret_cast<const uint4*>(p);
   const uint32_t w[4] = {u.x, u.y, u.z, u.w};
@@ -313,6 +324,11 @@ __device__ __forceinline__ void st8bf(bf16_t* p, const float (&v)[8]) {
   for (int q = 0; q < 4; ++q) w[q] = (uint32_t)from_f<bf16_t>(v[2 * q]).x | ((uint32_t)from_f<bf16_t>(v[2 * q + 1]).x << 16);
   *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
 }
+__device__ __forceinline__ void st8f(float* p, const float (&v)[8]) {
+  *reinterpret_cast<floatx4*>(p) = floatx4{v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<floatx4*>(p + 4) = floatx4{v[4], v[5], v[6], v[7]};
+}
+
 __device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
   const floatx4 a = *reinterpret_cast<const floatx4*>(p), b = *reinterpret_cast<const floatx4*>(p + 4);
 #pragma unroll
@@ -393,67 +409,109 @@ __global__ __launch_bounds__(256) void ln_fwd_bf16_kernel(const bf16_t* __restri
     }
 }
 
+// LDS bytes of ln_bwd_bf16_kernel: gamma + the column partials (dgamma, dbeta, sum dx) of the 8 half waves
+constexpr int ln_bwd_bf16_lds(int cols) { return (1 + 8 * 3) * cols * 4; }
+
 template <int NV>
-__global__ __launch_bounds__(256) void ln_bwd_bf16_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ xhat,
+__global__ __launch_bounds__(256, NV <= 3 ? 2 : 1) void ln_bwd_bf16_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ xhat,
                                                           const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                           bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
                                                           float* __restrict__ ws, int rows, int cols, float p_in,
                                                           float p_out, uint64_t seed, uint64_t off_in, uint64_t off_out,
                                                           int acc_res, int want_sum) {
-  __shared__ float red[4][1024];
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, l = lane & 31;
+  // eight half-wave rows per block step (one row per half wave and step), software-pipelined: the next row's
+  // dy / xhat loads (raw 16-B words) are issued before this row's arithmetic and stores (without it the loads
+  // sat idle through each row's reduction and stores, ~3.7 TB/s at 20,992 x 768).  To fit that pipeline in
+  // 2 waves per SIMD, the column partials of dgamma / dbeta / sum(dx) live in LDS (one private [3][cols]
+  // slice per half wave, read-modify-written per row) instead of 3 x 8 x NV registers, gamma is read from LDS
+  // (a global load in the row loop sat behind the prefetch in the in-order load counter), and xhat and the
+  // residual stay packed until used.
+  extern __shared__ float lnb_smem[];
+  float* gam_s = lnb_smem;
+  float* part = lnb_smem + cols;   // [8 half waves][3][cols]
+  const int lane = threadIdx.x & 63, l = lane & 31, hw = threadIdx.x >> 5;
   constexpr int nv = NV;
   const K3mDrop din = k3m_drop_init(seed, p_in), dout = k3m_drop_init(seed, p_out);
-  float pg[MAXV8][8], pb[MAXV8][8], px[MAXV8][8];
-#pragma unroll
-  for (int j = 0; j < MAXV8; ++j)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) pg[j][e] = pb[j][e] = px[j][e] = 0.f;
-  // eight half-wave rows per block step (one row per half wave and step: two rows per wave in flight, as
-  // the one-wave-per-row kernel's two-row steps, at half its registers for the loads)
+  for (int c = threadIdx.x; c < cols; c += 256) gam_s[c] = gamma[c];
+  for (int c = threadIdx.x; c < 24 * cols; c += 256) part[c] = 0.f;
+  __syncthreads();
+  float* pg = part + hw * 3 * cols;
+  float* pb = pg + cols;
+  float* px = pb + cols;
   const int S = gridDim.x * 8;
-  for (int row = blockIdx.x * 8 + (threadIdx.x >> 5); row < rows; row += S) {
+  const bf16_t* rsrc = acc_res ? dres : dy;
+  uint4 nd[MAXV8], nx[MAXV8];
+  int row = blockIdx.x * 8 + hw;
+  if (row < rows) {
     const long long base = (long long)row * cols;
-    float d[MAXV8][8], xv[MAXV8][8], old[MAXV8][8];
-    const bf16_t* rsrc = acc_res ? dres : dy;   // every load of the row issued before the arithmetic
 #pragma unroll
     for (int j = 0; j < nv; ++j) {
-      ld8bf(dy + base + (l + 32 * j) * 8, d[j]);
-      ld8bf(xhat + base + (l + 32 * j) * 8, xv[j]);
-      ld8bf(rsrc + base + (l + 32 * j) * 8, old[j]);
+      nd[j] = *reinterpret_cast<const uint4*>(dy + base + (l + 32 * j) * 8);
+      nx[j] = *reinterpret_cast<const uint4*>(xhat + base + (l + 32 * j) * 8);
     }
+  }
+  for (; row < rows; row += S) {
+    const long long base = (long long)row * cols;
+    float d[MAXV8][8];
+    uint4 cx[MAXV8], co[MAXV8];
+    const float rs = rstd[row];
+#pragma unroll
+    for (int j = 0; j < nv; ++j) {
+      unpack8bf(nd[j], d[j]);
+      cx[j] = nx[j];
+      co[j] = *reinterpret_cast<const uint4*>(rsrc + base + (l + 32 * j) * 8);   // used last
+    }
+    __builtin_amdgcn_sched_barrier(0);   // rstd and the residual ahead of the prefetch in the load counter
+    {
+      // unconditional (the last step re-reads a valid row): under a branch, the wait counts after it were
+      // those of the path without the prefetch, draining it
+      const long long nbase = (long long)min(row + S, rows - 1) * cols;
+#pragma unroll
+      for (int j = 0; j < nv; ++j) {
+        nd[j] = *reinterpret_cast<const uint4*>(dy + nbase + (l + 32 * j) * 8);
+        nx[j] = *reinterpret_cast<const uint4*>(xhat + nbase + (l + 32 * j) * 8);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < MAXV8; ++j)
       if (j < nv) {
         const int c = (l + 32 * j) * 8;
-        float g[8];
-        ld8f(gamma + c, g);
+        float g[8], xv[8], ag[8], ab[8];
+        ld8f(gam_s + c, g);
+        ld8f(pg + c, ag);
+        ld8f(pb + c, ab);
+        unpack8bf(cx[j], xv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float dd = d[j][e];
           if (p_out > 0.f) dd *= k3m_drop(dout, off_out + base + c + e);
           d[j][e] = dd;
-          pg[j][e] += dd * xv[j][e];
-          pb[j][e] += dd;
+          ag[e] += dd * xv[e];
+          ab[e] += dd;
           const float dxh = dd * g[e];
           s1 += dxh;
-          s2 += dxh * xv[j][e];
+          s2 += dxh * xv[e];
         }
+        st8f(pg + c, ag);
+        st8f(pb + c, ab);
       }
     const float m1 = half_sum(s1) / cols, m2 = half_sum(s2) / cols;
-    const float rs = rstd[row];
 #pragma unroll
     for (int j = 0; j < MAXV8; ++j)
       if (j < nv) {
         const int c = (l + 32 * j) * 8;
-        float g[8], ds[8], dr[8];
-        ld8f(gamma + c, g);
+        float g[8], ds[8], dr[8], xv[8];
+        ld8f(gam_s + c, g);
+        unpack8bf(cx[j], xv);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) ds[e] = (d[j][e] * g[e] - m1 - xv[j][e] * m2) * rs;
+        for (int e = 0; e < 8; ++e) ds[e] = (d[j][e] * g[e] - m1 - xv[e] * m2) * rs;
         if (acc_res) {
+          float old[8];
+          unpack8bf(co[j], old);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) dr[e] = ds[e] + old[j][e];
+          for (int e = 0; e < 8; ++e) dr[e] = ds[e] + old[e];
         } else {
 #pragma unroll
           for (int e = 0; e < 8; ++e) dr[e] = ds[e];
@@ -467,29 +525,24 @@ __global__ __launch_bounds__(256) void ln_bwd_bf16_kernel(const bf16_t* __restri
           st8bf(dx + base + c, ds);
         }
         if (want_sum) {   // the sum of dx as stored (bf16-rounded)
+          float ax[8];
+          ld8f(px + c, ax);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) px[j][e] += to_f(from_f<bf16_t>(ds[e]));
+          for (int e = 0; e < 8; ++e) ax[e] += to_f(from_f<bf16_t>(ds[e]));
+          st8f(px + c, ax);
         }
       }
   }
-  // the two half waves hold the same columns: fold them, then the 4 waves through LDS
-  for (int k = 0; k < (want_sum ? 3 : 2); ++k) {
+  // the block's slab: per column, the two half waves of each wave first, then the 4 waves in order (the
+  // order of the register version's shuffle + LDS fold)
+  __syncthreads();
+  for (int k = 0; k < (want_sum ? 3 : 2); ++k)
+    for (int c = threadIdx.x; c < cols; c += 256) {
+      float t[4];
 #pragma unroll
-    for (int j = 0; j < MAXV8; ++j)
-      if (j < nv) {
-        const int c = (l + 32 * j) * 8;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float v = k == 0 ? pg[j][e] : (k == 1 ? pb[j][e] : px[j][e]);
-          v += __shfl_xor(v, 32, 64);
-          if (lane < 32) red[w][c + e] = v;
-        }
-      }
-    __syncthreads();
-    for (int c = threadIdx.x; c < cols; c += 256)
-      ws[((long long)k * gridDim.x + blockIdx.x) * cols + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
-    __syncthreads();
-  }
+      for (int q = 0; q < 4; ++q) t[q] = part[(2 * q) * 3 * cols + k * cols + c] + part[(2 * q + 1) * 3 * cols + k * cols + c];
+      ws[((long long)k * gridDim.x + blockIdx.x) * cols + c] = t[0] + t[1] + t[2] + t[3];
+    }
 }
 
 // ------------------------------------------------------------------ embeddings
@@ -755,6 +808,17 @@ extern "C" int k3m_ln_fwd(const void* x, const void* res, const float* gamma, co
 // at least kLnRowsPerSlab rows per slab (per workgroup): at 4, a short LayerNorm (2,304 rows) wrote 512 x 3
 // slabs of cols fp32, more bytes than it reads; 8 measured 2,304 x 768 19.6 -> 17.1 us, 2,368 x 1,024 21.9 ->
 // 20.3 (backward + its reduction, fp32 and bf16 alike), no change on the long ones (profiles/r3_ln_bf16.txt)
+// ln_bwd_bf16_kernel's dynamic LDS exceeds the 64 KB default at cols = 1,024
+template <int NV>
+void ln_bwd_bf16_attr() {
+  static const bool done = [] {
+    (void)hipFuncSetAttribute((const void*)ln_bwd_bf16_kernel<NV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              ln_bwd_bf16_lds(NV * 256));
+    return true;
+  }();
+  (void)done;
+}
+
 const int kLnRowsPerSlab = k3m_env_int("K3M_LN_ROWS_PER_SLAB", 8);
 static int ln_bwd_slab_count(int rows) {
   return std::max(1, std::min(LN_BWD_BLOCKS, k3m_cdiv(rows, kLnRowsPerSlab)));
@@ -776,7 +840,8 @@ extern "C" int k3m_ln_bwd_slabs(const void* dy, const void* xhat, const float* r
   const int nv = cols >> 8;
   if (dtype == K3M_BF16 && kLnBf16Vec && rows >= LN_VEC_BWD_ROWS) {
 #define K3M_LNB16(NV_)                                                                                         \
-  hipLaunchKernelGGL(ln_bwd_bf16_kernel<NV_>, dim3(nb), dim3(256), 0, st, (const bf16_t*)dy,                  \
+  ln_bwd_bf16_attr<NV_>();                                                                                     \
+  hipLaunchKernelGGL(ln_bwd_bf16_kernel<NV_>, dim3(nb), dim3(256), ln_bwd_bf16_lds(cols), st, (const bf16_t*)dy,                  \
                       (const bf16_t*)xhat, rstd, gamma, (bf16_t*)dres, (bf16_t*)dx, ws, rows, cols, p_in, p_out, \
                       seed, off_in, off_out, acc_res, want_sum)
     K3M_LN_NV(K3M_LNB16);

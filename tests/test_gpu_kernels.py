@@ -119,6 +119,66 @@ def test_layernorm(dev, cols):
     assert _rel(xs, 1 + xr.grad.sum(0)) < 1e-4   # fused bias gradient of the producing Linear
 
 
+@pytest.mark.parametrize("cols,acc,alias", [(768, False, True), (768, True, False), (1024, True, False)])
+def test_layernorm_bwd_bf16_long(dev, cols, acc, alias):
+    """The software-pipelined half-wave bf16 backward (norm.hip ln_bwd_bf16_kernel, rows >= 16,384, LDS column
+    partials) against the LayerNorm backward in fp32 torch on the same bf16 inputs; 20,003 rows leave a ragged
+    last grid step.  Also reduced by the one-call k3m_ln_bwd (slab_batch_kernel)."""
+    from k3m_amd import ops
+    M = 20003
+    gen = torch.Generator(device="cpu").manual_seed(cols + acc)
+    dy = torch.randn(M, cols, generator=gen).to(dev).bfloat16()
+    xh = torch.randn(M, cols, generator=gen).to(dev).bfloat16()
+    rs = (0.5 + torch.rand(M, generator=gen)).to(dev)
+    g = (1 + 0.1 * torch.randn(cols, generator=gen)).to(dev)
+    old = torch.randn(M, cols, generator=gen).to(dev).bfloat16()
+    dres = old.clone()
+    dx = dres if alias else torch.empty_like(dres)
+    dg = torch.zeros(cols, device=dev)
+    db = torch.zeros(cols, device=dev)
+    xs = torch.zeros(cols, device=dev)
+    ops.ln_bwd(dy, xh, rs, g, dres, dx, dg, db, acc_res=acc, dxsum=xs)
+    d, x = dy.float(), xh.float()
+    dxh = d * g
+    ds = (dxh - dxh.mean(1, keepdim=True) - x * (dxh * x).mean(1, keepdim=True)) * rs[:, None]
+    ref = ds + old.float() if acc else ds
+    # bf16 outputs: one rounding of the fp32 value (2^-8 relative) on top of fp32 summation-order differences
+    assert _rel(dres.float(), ref) < 5e-3
+    if not alias:
+        assert _rel(dx.float(), ds) < 5e-3
+    assert _rel(dg, (d * x).sum(0)) < 1e-5
+    assert _rel(db, d.sum(0)) < 1e-5
+    assert _rel(xs, dx.float().sum(0)) < 1e-5   # the sum of dx as stored
+
+
+@pytest.mark.parametrize("nslab", [2, 7, 9, 20])
+def test_slab_reduce_batch_orders(dev, nslab):
+    """k3m_slab_reduce_batch's split-K (vec) path: out (+)= slab 0 + slab 1 + ... in that order, bit-exact
+    against the same left-to-right fp32 sum, for the slab counts the weight gradients use."""
+    import ctypes as C
+    from k3m_amd import _lib as L
+    cols = 768 * 3072 + 4
+    gen = torch.Generator(device="cpu").manual_seed(nslab)
+    ws = torch.randn(nslab, cols, generator=gen).to(dev)
+    out0 = torch.randn(cols, generator=gen).to(dev)
+    outs = [out0.clone(), torch.empty_like(out0)]
+    for acc, out in zip((1, 0), outs):
+        n = 1
+        wsp = (C.c_void_p * n)(ws.data_ptr())
+        op = (C.c_void_p * n)(out.data_ptr())
+        ns = (C.c_int * n)(nslab)
+        cs = (C.c_int * n)(cols)
+        ac = (C.c_int * n)(acc)
+        L.call("k3m_slab_reduce_batch", C.cast(wsp, C.c_void_p), C.cast(op, C.c_void_p), C.cast(ns, C.c_void_p),
+               C.cast(cs, C.c_void_p), C.cast(ac, C.c_void_p), n, L.stream())
+    torch.cuda.synchronize()
+    ref = ws[0].clone()
+    for k in range(1, nslab):
+        ref += ws[k]
+    assert torch.equal(outs[1], ref)
+    assert torch.equal(outs[0], out0 + ref)
+
+
 def test_dropout_ln_regenerates_mask(dev):
     from k3m_amd import ops
     M, cols = 512, 768
