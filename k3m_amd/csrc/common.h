@@ -192,3 +192,26 @@ static inline bool k3m_env_flag(const char* name, bool dflt) {   // "0" = off, a
   const char* e = std::getenv(name);
   return e ? !(e[0] == '0') : dflt;
 }
+
+// Longest-first order of a grouped launch's problems (stable; by the k length of one work unit, k / splitk).
+// The persistent walks deal work units to the CUs round-robin in problem order, so a group mixing k = 1,024
+// and k = 3,072 problems left some CUs three long units and others a short one; longest first, the last
+// partial wave holds the short units (LPT scheduling).  Outputs are unchanged: every unit computes the same
+// tile over the same k range in the same order.  K3M_GROUP_LPT=0 keeps the caller's order (A/B knob).
+static inline long long k3m_unit_k(const K3mGemm& g) { return g.splitk > 1 ? (g.k + g.splitk - 1) / g.splitk : g.k; }
+static inline void k3m_lpt_order(K3mGemm* g, bool* flag, int n) {
+  static const bool on = k3m_env_flag("K3M_GROUP_LPT", false);
+  if (!on) return;
+  for (int i = 1; i < n; ++i) {
+    const K3mGemm gi = g[i];
+    const bool fi = flag[i];
+    const long long wi = k3m_unit_k(gi);
+    int j = i - 1;
+    for (; j >= 0 && k3m_unit_k(g[j]) < wi; --j) {
+      g[j + 1] = g[j];
+      flag[j + 1] = flag[j];
+    }
+    g[j + 1] = gi;
+    flag[j + 1] = fi;
+  }
+}

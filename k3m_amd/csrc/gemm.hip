@@ -331,6 +331,7 @@ extern "C" int k3m_gemm_grouped(const K3mGemm* gs_in, int count, hipStream_t st)
     K3M_ARG((g.epilogue != K3M_EPI_BIAS_GELU && g.epilogue != K3M_EPI_DGELU) || g.aux);
   }
   if (live == 0) return 0;
+  k3m_lpt_order(grp.g, live_slabs, live);
   const bool ak = g0.a_trans == 0, bk = g0.b_trans == 1;
   // same tile rule as k3m_gemm, over the whole grid (prefer_256x256)
   const long long w128 = (nb128 + 255) / 256, w256 = (nb256 + 255) / 256;

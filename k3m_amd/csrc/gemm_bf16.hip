@@ -720,6 +720,7 @@ int k3m_gemm_bf16_grouped_impl(const K3mGemm* gs, int count, hipStream_t st, boo
   }
   *handled = true;
   if (live == 0) return 0;
+  k3m_lpt_order(grp.g, live_slabs, live);
   const bool t256 = big_prefers_256(nb256);
   int nb = 0;
   for (int i = 0; i < live; ++i) {

@@ -217,31 +217,85 @@ SPLITK_COST_BF16 = float(os.environ.get("K3M_SPLITK_COST_BF16", "0.02"))
 SPLITK_MINK_F32 = int(os.environ.get("K3M_SPLITK_MINK_F32", "1024"))
 
 
-def _splitk(m, n, k, dtype=torch.float32):
+# Under-filled fp32 weight gradients (K3M_SPLITK_FILL, A/B knob): an ungrouped split-K GEMM whose split under
+# the default minimum k per slice leaves half of the 256 CUs idle or more (the image-stream 1,024 x 1,024 x 4,736
+# projections: 128 work units) may use slices of half that depth, none of them empty.  Grouped GEMMs share one
+# grid with the group's others and keep the default (a global minimum of 512 cost 0.6 % of the fp32 step,
+# profiles/r4b_ab_mink.txt).  bf16 (a slice's MFMA time ~1/6 of the x6 one, so the extra slabs' traffic
+# weighs more): _bf16_fill_split's time model, for splits leaving half of the CUs idle or more.
+SPLITK_FILL = os.environ.get("K3M_SPLITK_FILL", "0") != "0"
+
+
+def _split_cost_min(tiles, k, kmin, cost_per, bk, smax=32, nonempty=False):
+    best, best_cost = 1, float("inf")
+    for s in range(1, min(smax, k // kmin) + 1):
+        if nonempty and s > 1:
+            kt = (k + bk - 1) // bk
+            per = (kt + s - 1) // s
+            if per * (s - 1) >= kt:   # the last slice would be empty
+                continue
+        cost = ((tiles * s + 255) // 256) / s * (1.0 + cost_per * s)
+        if cost < best_cost - 1e-9:
+            best, best_cost = s, cost
+    return best, best_cost
+
+
+B16_MIN256 = int(os.environ.get("K3M_B16_256", "128"))   # gemm_bf16.hip big_prefers_256 (same env knob)
+
+
+def _bf16_fill_split(m, n, k, s0):
+    """An ungrouped bf16 weight gradient whose default split leaves half of the CUs idle or more (the image-stream
+    1,024 x 1,024 x 4,736 projections: 128 units of 256 x 128): the split minimising a time model of waves x
+    tile MFMA time (at 20 % of the per-CU peak: the split-4 launch measured 61 us, profiles/r4b_gemm_calls_cfg3.txt,
+    for 52 in this model) + the slabs' HBM write and read (5 TB/s), with the tile the
+    library will pick (256 x 128 below B16_MIN256 units of 256 x 256), no empty slice, >= 4 k-tiles per slice.
+    Kept only if the model gains 20 %."""
+    kt = (k + 63) // 64
+
+    def model(s):
+        t256 = ((m + 255) // 256) * ((n + 255) // 256)
+        nb256 = t256 * s
+        tbn = 256 if nb256 >= B16_MIN256 else 128
+        units = ((m + 255) // 256) * ((n + tbn - 1) // tbn) * s
+        per = (kt + s - 1) // s * 64
+        mfma = 256.0 * tbn * per * 2 / (2.5e15 / 256 * 0.2)
+        slab = (s * m * n * 8.0) / 5e12 if s > 1 else 0.0
+        return (units + 255) // 256 * mfma + slab
+
+    best, best_t = s0, model(s0)
+    for s in range(2, min(32, kt // 4) + 1):
+        per = (kt + s - 1) // s
+        if per * (s - 1) >= kt:
+            continue
+        t = model(s)
+        if t < best_t:
+            best, best_t = s, t
+    return best if best_t < 0.8 * model(s0) else s0
+
+
+def _splitk(m, n, k, dtype=torch.float32, grouped=False):
     """K-split of a weight-gradient GEMM (C[m,n] summed over k ~ 20k rows): enough blocks to fill
     the 256 CUs in whole waves.  fp32 (bf16x6 kernel) tiles are 256x128 at one block per CU;
-    bf16 tiles are 128x128 at two per CU."""
+    bf16 tiles are 256x256 at one block per CU."""
     if dtype == torch.float32 and F32_ALGO == L.F32_SPLIT_BF16X6:
         tiles = ((m + 255) // 256) * ((n + 127) // 128)
         if tiles >= 200 or k < 2048:
             return 1
         # minimise (waves of 256 blocks) x (k per split), plus ~1% per split for the slab reduction
-        best, best_cost = 1, float("inf")
-        for s in range(1, min(32, k // SPLITK_MINK_F32) + 1):
-            cost = ((tiles * s + 255) // 256) / s * (1.0 + SPLITK_COST_F32 * s)
-            if cost < best_cost - 1e-9:
-                best, best_cost = s, cost
+        best, cost = _split_cost_min(tiles, k, SPLITK_MINK_F32, SPLITK_COST_F32, 32)
+        if SPLITK_FILL and not grouped and tiles * best <= 128:
+            s2, c2 = _split_cost_min(tiles, k, SPLITK_MINK_F32 // 2, SPLITK_COST_F32, 32, nonempty=True)
+            if c2 < cost - 1e-9:
+                best = s2
         return best
     if dtype == torch.bfloat16 and k % 64 == 0 and m % 8 == 0 and n % 8 == 0:
         # the large-tile bf16 kernel (gemm_b16_tile.h): 256x256 blocks, one per CU; >= 16 k-tiles per split
         tiles = ((m + 255) // 256) * ((n + 255) // 256)
         if tiles >= 192 or k < 2048:
             return 1
-        best, best_cost = 1, float("inf")
-        for s in range(1, min(32, k // 1024) + 1):
-            cost = ((tiles * s + 255) // 256) / s * (1.0 + SPLITK_COST_BF16 * s)
-            if cost < best_cost - 1e-9:
-                best, best_cost = s, cost
+        best = _split_cost_min(tiles, k, 1024, SPLITK_COST_BF16, 64)[0]
+        if SPLITK_FILL and not grouped and tiles * best <= 64:   # 256 x 256 tiles; <= 128 units of 256 x 128
+            best = _bf16_fill_split(m, n, k, best)
         return best
     tiles = ((m + 127) // 128) * ((n + 127) // 128)
     if tiles >= 384 or k < 1024:
@@ -255,7 +309,7 @@ def linear_wgrad(dy, x, gW, gb=None, alpha=1.0):
     dy's producer).  dy [M,N], x [M,K], gW [N,K] fp32."""
     M, N = dy.shape
     K = x.shape[1]
-    s = _splitk(N, K, M, dy.dtype)
+    s = _splitk(N, K, M, dy.dtype, grouped=_grouper is not None)
     ws = torch.empty((s * N * K,), dtype=torch.float32, device=dy.device) if s > 1 else None
     epi = L.EPI_NONE
     if s > 1 and DEFER and _deferred is not None and alpha == 1.0 and gW.is_contiguous() and _deferred.active_here():

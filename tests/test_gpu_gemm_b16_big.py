@@ -71,6 +71,7 @@ def test_dgrad_kc_mn(dev, m, n, k):
 
 
 @pytest.mark.parametrize("n,k,m,splitk", [(3072, 768, 20992, 1), (3072, 768, 20992, 7), (1024, 1024, 4736, 4),
+                                          (1024, 1024, 4736, 7),   # ops._splitk fill rule: 256 x 128 tiles, last slice short
                                           (768, 768, 2304, 3)])
 def test_wgrad_mn_mn(dev, n, k, m, splitk):
     """gW[n,k] += alpha dy^T x (both MN-contiguous), fp32 C, split-K slabs."""

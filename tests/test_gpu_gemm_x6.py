@@ -69,6 +69,16 @@ def test_x6_splitk_256x256(dev, at, bt):
     _case(dev, 3072, 768, 20000, at, bt, splitk=7)
 
 
+def test_x6_splitk_fill_rule(dev):
+    """The image-stream weight gradient (1,024 x 1,024 over 4,736 rows) under ops._splitk's fill rule: 8 slices
+    of 592 rows (the default minimum would give 4, half the CUs idle); the last slice shorter, none empty."""
+    from k3m_amd import ops
+    s = ops._splitk(1024, 1024, 4736, torch.float32)
+    assert s == (8 if ops.SPLITK_FILL else 4)
+    assert ops._splitk(1024, 1024, 4736, torch.float32, grouped=True) == 4
+    _case(dev, 1024, 1024, 4736, 1, 0, splitk=s)
+
+
 def test_x6_epilogues_match_torch(dev):
     from k3m_amd import ops, _lib as L
     x = torch.randn(2048, 768, device=dev)
