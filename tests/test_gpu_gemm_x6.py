@@ -119,11 +119,14 @@ def test_x6_beta_all_tiles(dev, m, n, k, at, bt):
         assert err < 2e-5 * float(ref.abs().max()), err
 
 
-def test_grouped_matches_individual():
-    """k3m_gemm_grouped (one grid over several problems) is bit-identical to launching each problem
-    through k3m_gemm: same tile computation, split-K slabs and epilogues."""
+def test_grouped_matches_individual(monkeypatch):
+    """k3m_gemm_grouped (one grid over several problems, in any problem order: K3M_GROUP_LPT) is bit-identical to
+    launching each problem through k3m_gemm with the same split: same tile computation, split-K slabs and
+    epilogues.  (ops._splitk's fill rule gives an UNgrouped under-filled weight gradient more k-slices than the
+    grouped call, a different fp32 summation order; it is held off here.)"""
     import torch
     from k3m_amd import ops, _lib as L
+    monkeypatch.setattr(ops, "SPLITK_FILL", False)
     dev = torch.device("cuda")
     torch.manual_seed(0)
     cases = [  # (m, n, k, epi) nt forward problems of the co-attention blocks, ragged edges included
