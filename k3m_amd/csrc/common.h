@@ -200,7 +200,7 @@ static inline bool k3m_env_flag(const char* name, bool dflt) {   // "0" = off, a
 // tile over the same k range in the same order.  K3M_GROUP_LPT=0 keeps the caller's order (A/B knob).
 static inline long long k3m_unit_k(const K3mGemm& g) { return g.splitk > 1 ? (g.k + g.splitk - 1) / g.splitk : g.k; }
 static inline void k3m_lpt_order(K3mGemm* g, bool* flag, int n) {
-  static const bool on = k3m_env_flag("K3M_GROUP_LPT", false);
+  static const bool on = k3m_env_flag("K3M_GROUP_LPT", true);
   if (!on) return;
   for (int i = 1; i < n; ++i) {
     const K3mGemm gi = g[i];

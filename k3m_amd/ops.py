@@ -223,7 +223,7 @@ SPLITK_MINK_F32 = int(os.environ.get("K3M_SPLITK_MINK_F32", "1024"))
 # grid with the group's others and keep the default (a global minimum of 512 cost 0.6 % of the fp32 step,
 # profiles/r4b_ab_mink.txt).  bf16 (a slice's MFMA time ~1/6 of the x6 one, so the extra slabs' traffic
 # weighs more): _bf16_fill_split's time model, for splits leaving half of the CUs idle or more.
-SPLITK_FILL = os.environ.get("K3M_SPLITK_FILL", "0") != "0"
+SPLITK_FILL = os.environ.get("K3M_SPLITK_FILL", "1") != "0"
 
 
 def _split_cost_min(tiles, k, kmin, cost_per, bk, smax=32, nonempty=False):
