@@ -195,7 +195,8 @@ def pmc_traffic(key, kernel):
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        names = d.get("kernel_names") or [d.get("kernel", "")]
+        # rocprofv3 names keep the "(anonymous namespace)::" of the kernels' translation units
+        names = [n.replace("(anonymous namespace)::", "") for n in (d.get("kernel_names") or [d.get("kernel", "")])]
         if tuple(d.get("shape") or ()) == tuple(key) and d.get("traffic_bytes") and any(kernel in n for n in names):
             return int(d["traffic_bytes"]), os.path.relpath(path, HERE)
     return None, None
