@@ -758,7 +758,9 @@ int grid_for(long long n) { return (int)std::min<long long>((n + 255) / 256, 409
 // ones (2,304 rows) are 5-20 % slower.  A/B knob: K3M_LN_BF16_VEC=0 keeps every bf16 LayerNorm on the
 // one-wave-per-row kernels.
 const bool kLnBf16Vec = k3m_env_flag("K3M_LN_BF16_VEC", true);
-constexpr int LN_VEC_FWD_ROWS = 4096, LN_VEC_BWD_ROWS = 16384;
+constexpr int LN_VEC_FWD_ROWS = 4096;
+// fewest rows for the half-wave bf16 backward (A/B knob K3M_LN_VEC_BWD_ROWS)
+const int kLnVecBwdRows = k3m_env_int("K3M_LN_VEC_BWD_ROWS", 16384);
 
 }  // namespace
 
@@ -838,7 +840,7 @@ extern "C" int k3m_ln_bwd_slabs(const void* dy, const void* xhat, const float* r
   if (rows == 0) return 0;
   const int nb = ln_bwd_slab_count(rows);
   const int nv = cols >> 8;
-  if (dtype == K3M_BF16 && kLnBf16Vec && rows >= LN_VEC_BWD_ROWS) {
+  if (dtype == K3M_BF16 && kLnBf16Vec && rows >= kLnVecBwdRows) {
 #define K3M_LNB16(NV_)                                                                                         \
   ln_bwd_bf16_attr<NV_>();                                                                                     \
   hipLaunchKernelGGL(ln_bwd_bf16_kernel<NV_>, dim3(nb), dim3(256), ln_bwd_bf16_lds(cols), st, (const bf16_t*)dy,                  \
