@@ -100,10 +100,14 @@ __device__ __forceinline__ void split4(const floatx4 v, u32x2v& h, u32x2v& m, u3
 
 template <bool KC, int TILE, int BK, int NT>
 struct Stage {
-  // KC: TILE*BK/4 float4; MN: (BK/4)*(TILE/4) blocks of 4(k) x 4(mn) = 4 float4 each
-  static constexpr int NV = KC ? TILE * BK / 4 : BK * TILE / 16;
+  // TILE*BK/4 float4 per k-tile, spread over every thread of the block: KC = 4 consecutive k of one
+  // row, MN = 4 consecutive mn of one k row.  (Round 4 and earlier staged MN operands as 4(k) x 4(mn)
+  // blocks, which left half the threads of a 256-wide tile idle: those waves split nothing while their
+  // SIMD partners split twice their share, and the extra 8 staging VGPRs per set made the input-gradient
+  // walk spill inside its main loop.)
+  static constexpr int NV = TILE * BK / 4;
   static constexpr int NB = (NV + NT - 1) / NT;
-  static constexpr int NR = KC ? NB : 4 * NB;
+  static constexpr int NR = NB;
   floatx4 r[NR];
 };
 
@@ -127,9 +131,9 @@ struct Src {
         kq[b] = 4 * q;
         p[b] = base + (long long)min(mn0 + row, MN - 1) * ld + kbeg + 4 * q;
       } else {
-        const int qm = idx % (TILE / 4), g4 = idx / (TILE / 4);
-        kq[b] = 4 * g4;
-        p[b] = base + (long long)(kbeg + 4 * g4) * ld + max(0, min(mn0 + 4 * qm, MN - 4));
+        const int qm = idx % (TILE / 4), kr = idx / (TILE / 4);
+        kq[b] = kr;
+        p[b] = base + (long long)(kbeg + kr) * ld + max(0, min(mn0 + 4 * qm, MN - 4));
       }
     }
   }
@@ -154,8 +158,7 @@ __device__ __forceinline__ void load_full(Src<KC, TILE, BK, NT>& src, long long 
       s.r[b] = *reinterpret_cast<const floatx4*>(src.p[b]);
       src.p[b] += adv ? BK : 0;
     } else {
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) s.r[4 * b + kk] = *reinterpret_cast<const floatx4*>(src.p[b] + kk * ld);
+      s.r[b] = *reinterpret_cast<const floatx4*>(src.p[b]);
       src.p[b] += adv ? BK * ld : 0;
     }
   }
@@ -174,9 +177,7 @@ __device__ __forceinline__ void load_tail(const Src<KC, TILE, BK, NT>& src, long
     if constexpr (KC) {
       s.r[b] = src.kq[b] < krem ? *reinterpret_cast<const floatx4*>(src.p[b]) : z;
     } else {
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
-        s.r[4 * b + kk] = src.kq[b] + kk < krem ? *reinterpret_cast<const floatx4*>(src.p[b] + kk * ld) : z;
+      s.r[b] = src.kq[b] < krem ? *reinterpret_cast<const floatx4*>(src.p[b]) : z;
     }
   }
 }
@@ -206,16 +207,13 @@ __device__ __forceinline__ void store_tile(__bf16* __restrict__ lds, const Stage
     for (int b = 0; b < Stage<KC, TILE, BK, NT>::NB; ++b) {
       const int idx = t + NT * b;
       if (NV % NT != 0 && idx >= NV) break;
-      const int qm = idx % Q, g4 = idx / Q;
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {   // k row 4 g4 + kk, columns 4 qm .. 4 qm + 3
-        const int off = mn_off<TILE>(4 * g4 + kk, qm >> 1) + 4 * (qm & 1);
-        u32x2v h, m, l;
-        split4(s.r[4 * b + kk], h, m, l);
-        *reinterpret_cast<u32x2v*>(lds + off) = h;
-        *reinterpret_cast<u32x2v*>(lds + PL + off) = m;
-        *reinterpret_cast<u32x2v*>(lds + 2 * PL + off) = l;
-      }
+      const int qm = idx % Q, kr = idx / Q;   // k row kr, columns 4 qm .. 4 qm + 3
+      const int off = mn_off<TILE>(kr, qm >> 1) + 4 * (qm & 1);
+      u32x2v h, m, l;
+      split4(s.r[b], h, m, l);
+      *reinterpret_cast<u32x2v*>(lds + off) = h;
+      *reinterpret_cast<u32x2v*>(lds + PL + off) = m;
+      *reinterpret_cast<u32x2v*>(lds + 2 * PL + off) = l;
     }
   }
 }
