@@ -19,9 +19,13 @@ Eligible: one process (no DDP all-reduce), accum_steps == 1, the label-count hin
 inside the step), the default warmup_linear schedule, the pretraining objective 2, the built-in AdamW.
 A step is captured when the same key (batch shapes, dtypes, label counts, dropout / overlap mode) came
 twice in a row; one graph is kept (a new key frees the old one), so a loader whose label counts change
-every batch simply stays eager.  The outputs returned by a replayed step are the graph's static tensors,
-overwritten by the next replay (clone what must outlive it).
+every batch simply stays eager.  A replayed step returns copies of its small outputs (the loss and the
+per-task losses), which outlive the next replay; larger outputs (logit-sized tensors) are the graph's static
+tensors, overwritten by the next replay (clone what must outlive it).  A capture that fails (an op that
+cannot be captured, a host sync on an untested path) is dropped with a warning and that key runs eagerly.
 """
+import warnings
+
 import numpy as np
 import torch
 
@@ -45,10 +49,10 @@ class AdamTable(object):
 
     RING = 3
 
-    def __init__(self, device):
+    def __init__(self, device, rows=256):
         self.device = device
         self.mult, self.wd, self.flags = [], [], None
-        self.dev = torch.zeros((256, 4), dtype=torch.float32, device=device)   # rows are 16-B aligned
+        self.dev = torch.zeros((max(int(rows), 1), 4), dtype=torch.float32, device=device)   # rows 16-B aligned
         self.host = None
 
     def row(self, mult, wd, flags):
@@ -91,6 +95,8 @@ class AdamTable(object):
 class StepGraph(object):
     """One captured step: static inputs, the graph, its outputs and the per-replay device scalars."""
 
+    SMALL = 4096   # outputs up to this many elements are returned as copies (loss terms, counters)
+
     def __init__(self, tr, batch):
         eng = tr.engine
         dev = eng.fp.device
@@ -98,7 +104,9 @@ class StepGraph(object):
         self.hint = tuple(int(x) for x in batch["_label_counts"])
         self.static = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in batch.items()}
         self.seed = torch.zeros((1,), dtype=torch.int64, device=dev)   # the step's seed word (outside the pool)
-        self.table = AdamTable(dev)
+        # one row per AdamW launch the step can issue: the sweep's runs or the per-block runs of the overlap
+        rows = max(len(tr.runs), sum(len(r) for r in getattr(tr, "block_runs", {}).values()))
+        self.table = AdamTable(dev, rows)
         torch.cuda.synchronize(dev)
         self.graph = torch.cuda.CUDAGraph()
         eng.graph_seed = self.seed.data_ptr()
@@ -128,11 +136,12 @@ class StepGraph(object):
         self.graph.replay()
         if self.counts is not None:
             eng._verify_hint(self.hint, self.counts)
+        out = {k: (v.clone() if torch.is_tensor(v) and v.numel() <= self.SMALL else v) for k, v in self.out.items()}
         if tr.watch is not None:
-            tr.watch.push(tr.global_step, self.out["loss"])
+            tr.watch.push(tr.global_step, out["loss"])
         tr.global_step += 1
         eng.step_count += 1
-        return self.out
+        return out
 
 
 class StepGraphs(object):
@@ -167,7 +176,19 @@ class StepGraphs(object):
         self.tr.engine.check_hints()   # a completed label-count check that failed raises before any update
         self.graph = None              # one graph: free the previous one's pool first
         torch.cuda.empty_cache()
-        self.graph = StepGraph(self.tr, batch)
+        try:
+            g = StepGraph(self.tr, batch)
+        except Exception as e:   # noqa: BLE001 - any capture failure falls back to the eager step
+            # nothing captured ran on the device and the capture body changes no host counters (count=False),
+            # so the eager step below is the step this call would have been
+            self.tr.engine.captured_counts = None
+            torch.cuda.synchronize()
+            self.decided[key] = "eager"
+            self.last_decision = {"mode": "eager", "capture_failed": "%s: %s" % (type(e).__name__, e)}
+            warnings.warn("k3m: hipGraph capture of the step failed (%s: %s); this batch shape runs eagerly"
+                          % (type(e).__name__, e))
+            return None
+        self.graph = g
         self.graph_key = key
         self.captures += 1
         self.replays += 1

@@ -125,8 +125,11 @@ class BertForMultiModalPreTraining_tri_stru(nn.Module):
         self.engine = eng
         for n in self._names:
             key = n.replace(".", "__")
-            grad = getattr(self, key).grad
-            p = nn.Parameter(eng.fp.p[n], requires_grad=True)
+            old_p = getattr(self, key)
+            grad = old_p.grad
+            # keep the driver's --freeze choice (train_concap_struc.py:255-257 runs before .half() at :300): the
+            # optimizer groups are built from requires_grad (:371), so that flag is what keeps a tensor frozen
+            p = nn.Parameter(eng.fp.p[n], requires_grad=old_p.requires_grad)
             self._parameters[key] = p
             if grad is not None:
                 p.grad = eng.fp.g[n]

@@ -245,6 +245,48 @@ def test_half_switches_to_bf16_mode(dev):
     assert gq is not None and torch.isfinite(gq).all() and float(gq.abs().max()) > 0
 
 
+def test_half_keeps_frozen_parameters(dev):
+    """--freeze then --fp16 (train_concap_struc.py:245-257, then model.half() at :300, then the optimizer groups
+    from ``value.requires_grad`` at :371): half() keeps each parameter's requires_grad, so an optimizer built the
+    driver's way leaves the frozen embeddings / text layers bit-identical after a step while the rest move."""
+    from vilbert_k3m.vilbert_k3m import BertForMultiModalPreTraining_tri_stru
+    from pytorch_transformers.optimization import AdamW
+    from k3m_amd.weights import param_values
+    g = load_case("bs2_hard")
+    cfg = case_config(g)
+    model = BertForMultiModalPreTraining_tri_stru(cfg, device=dev)
+    vals = param_values(cfg, int(g["weight_seed"]))
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()})
+    freeze = 1   # the driver's --freeze 1: embeddings and text layers 0..1
+
+    def frozen(n):
+        return "embeddings" in n or (n.startswith("encoder.layer.") and int(n.split(".")[2]) <= freeze)
+    for n, p in model.named_parameters():
+        if frozen(n):
+            p.requires_grad = False
+    model.half()
+    named = list(model.named_parameters())
+    assert any(frozen(n) for n, _ in named)
+    for n, p in named:
+        assert p.requires_grad == (not frozen(n)), n
+    before = {n: p.detach().clone() for n, p in named}
+    opt = AdamW([p for _, p in named if p.requires_grad], lr=1e-3, eps=1e-8, betas=(0.9, 0.98))
+    model.train()
+    tb = {k: v.to(dev) for k, v in case_batch(g).items()}
+    noise = {k: v.to(dev) for k, v in case_noise(g).items()}
+    ent, val = torch.from_numpy(g["ent_neg"]), torch.from_numpy(g["val_neg"])
+    outs = _driver_forward(model, tb, dev, noise, ent, val)
+    (outs[0] + outs[1] + outs[3] + outs[9]).backward()
+    opt.step()
+    moved = 0
+    for n, p in model.named_parameters():
+        if frozen(n):
+            assert torch.equal(p.detach(), before[n]), n
+        elif not torch.equal(p.detach(), before[n]):
+            moved += 1
+    assert moved > 100
+
+
 def test_unequal_mlm_loss_weights(dev):
     """A caller's  a*mlm_t + b*mlm_pv  (the reference sums them with weight 1, train_concap_struc.py:531-533): the
     shared decoder's text and PV gradient rows take their own upstream weights (k3m_scale_rows_by_slot), so the

@@ -162,3 +162,38 @@ def test_graph_step_matches_eager(dev, dtype):
     tb.finish()
     print("issue ms (host, step call): eager %s  graph %s" % (["%.1f" % x for x in eager_ms],
                                                               ["%.1f" % x for x in graph_ms]))
+
+
+def test_graph_outputs_outlive_replay_and_capture_failure_falls_back(dev):
+    """(a) the loss a replayed step returns is a copy, so a caller that keeps it across steps (deferred
+    logging) reads its own step's value; (b) a capture that raises is dropped with a warning and the step runs
+    eagerly (no exception out of Trainer.step), and that key stays eager."""
+    from k3m_amd.config import pretrain_config
+    from k3m_amd.engine import label_counts
+    from k3m_amd.synthetic import synthetic_batch
+    from k3m_amd.trainer import Trainer
+    cfg = pretrain_config(CFG_PATH)
+    batch = synthetic_batch(cfg, 2, dev, seed=5)
+    batch["_label_counts"] = label_counts(batch)
+    tr = Trainer(cfg, dev, lr=1e-3, warmup_steps=0, total_steps=20, seed=3)
+    tr.graph = True
+    kept = [tr.step(batch)["loss"] for _ in range(4)]   # eager, capture + replay, replay, replay
+    vals = [float(x) for x in kept]
+    assert tr._graphs.captures == 1 and tr._graphs.replays == 3
+    assert len(set(vals)) == 4, vals   # each step's own loss (parameters moved between steps)
+    assert kept[2].data_ptr() != kept[3].data_ptr()
+
+    tr2 = Trainer(cfg, dev, lr=1e-3, warmup_steps=0, total_steps=20, seed=3)
+    tr2.graph = True
+    real = tr2._device_step
+
+    def broken(b):
+        real(b)
+        raise RuntimeError("injected capture failure")
+    tr2._device_step = broken
+    with pytest.warns(UserWarning, match="capture of the step failed"):
+        outs = [float(tr2.step(batch)["loss"]) for _ in range(3)]
+    assert tr2._graphs.captures == 0 and tr2._graphs.graph is None
+    assert tr2.global_step == 3 and all(np.isfinite(outs))
+    assert tr2._graphs.last_decision["mode"] == "eager" and "injected" in tr2._graphs.last_decision["capture_failed"]
+    np.testing.assert_allclose(outs, vals[:3], rtol=1e-5)   # the eager fallback trains exactly like tr
