@@ -164,6 +164,25 @@ int k3m_flash_attn_bwd(const void* dctx, long long ldc, const void* o, long long
                        int nseq, int lq, int lk, int nh, int hd, float scale, float p_drop, uint64_t seed,
                        uint64_t off, hipStream_t stream);
 
+/* bf16 flash attention for sequences longer than 128, up to max_position_embeddings = 512
+ * (config/bert_base_6layer_6conect.json:8; the PV stream of BASELINE configs[4] at 320 tokens, fine-tuning PV 256):
+ * same semantics, LSE layout and dropout counters as k3m_flash_attn_fwd / _bwd, any lq, lk in [1, 512], head dim
+ * 64, 96 or 128, nothing of size lq x lk in HBM (attention_flash_long.hip).  Replaces the exact-fp32
+ * k3m_attn_long_* path of the bf16 encoder (BertSelfAttention :439-475, BertBiAttention :753-838,
+ * BertBiAttention_two_text :904-965).  The backward takes a workspace of k3m_flash_attn_long_ws_bytes(...) bytes
+ * (16-B aligned): D = rowsum(dO o O) and, when the keys of a head exceed one workgroup, fp32 dQ partials reduced
+ * in a fixed order (deterministic); *bytes receives the size.  Rows as in k3m_flash_attn_fwd; dq needs 8-B aligned
+ * rows (lddq % 4 == 0). */
+int k3m_flash_attn_long_fwd(const void* q, long long ldq, const void* k, long long ldk, const void* v, long long ldv,
+                            const float* kmask, void* ctx, long long ldc, float* lse, int nseq, int lq, int lk, int nh,
+                            int hd, float scale, float p_drop, uint64_t seed, uint64_t off, hipStream_t stream);
+int k3m_flash_attn_long_ws_bytes(int nseq, int lq, int lk, int nh, int hd, long long* bytes);
+int k3m_flash_attn_long_bwd(const void* dctx, long long ldc, const void* o, long long ldo, const void* q, long long ldq,
+                            const void* k, long long ldk, const void* v, long long ldv, const float* kmask,
+                            const float* lse, void* dq, void* dk, void* dv, long long lddq, long long lddk,
+                            long long lddv, void* ws, long long ws_bytes, int nseq, int lq, int lk, int nh, int hd,
+                            float scale, float p_drop, uint64_t seed, uint64_t off, hipStream_t stream);
+
 /* Elementwise: out = g * gelu'(pre) (backward of the MLM/image head transforms :1795-1818). */
 int k3m_dgelu(const void* g, const void* pre, void* out, long long n, int dtype, hipStream_t stream);
 

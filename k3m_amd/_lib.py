@@ -52,6 +52,11 @@ SIGNATURES = {
                            vp],
     "k3m_flash_attn_bwd": [vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, vp, vp, vp, vp, i64, i64, i64, i32, i32,
                            i32, i32, i32, f32, f32, u64, u64, vp],
+    "k3m_flash_attn_long_fwd": [vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, i32, f32, f32, u64,
+                                u64, vp],
+    "k3m_flash_attn_long_ws_bytes": [i32, i32, i32, i32, i32, vp],
+    "k3m_flash_attn_long_bwd": [vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, vp, vp, vp, vp, i64, i64, i64, vp, i64,
+                                i32, i32, i32, i32, i32, f32, f32, u64, u64, vp],
     "k3m_dgelu": [vp, vp, vp, i64, i32, vp],
     "k3m_gather_rows": [vp, i64, vp, i32, i32, vp, i64, i32, vp],
     "k3m_scatter_add_rows": [vp, i64, vp, i32, i32, vp, i64, i32, vp],

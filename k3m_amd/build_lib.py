@@ -7,7 +7,7 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libk3m_hip.so")
-SOURCES = ["gemm.hip", "gemm_x6p.hip", "gemm_bf16.hip", "norm.hip", "attention.hip", "attention_bf16.hip", "loss.hip", "fusion.hip", "struct.hip", "adamw.hip", "data.hip", "align.hip", "attention_long.hip"]
+SOURCES = ["gemm.hip", "gemm_x6p.hip", "gemm_bf16.hip", "norm.hip", "attention.hip", "attention_bf16.hip", "loss.hip", "fusion.hip", "struct.hip", "adamw.hip", "data.hip", "align.hip", "attention_long.hip", "attention_flash_long.hip"]
 # -fno-slp-vectorize: no packed-f32 (v_pk_*_f32) code from paired scalar math.  Beside MFMAs packed f32
 # VALU costs more than the scalar pair (MI355X_MICROARCH.md cycle constants), and in the GEMM epilogues
 # the packed alpha/beta form  v_pk_fma_f32 s[alpha:beta], op_sel  dropped the beta*C term for
@@ -27,7 +27,7 @@ def build(force=False, jobs=8, verbose=False):
     srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
     objdir = os.path.join(HERE, "build")
     os.makedirs(objdir, exist_ok=True)
-    deps = [os.path.join(CSRC, "common.h"), os.path.join(CSRC, "gemm_f32_tile.h"), os.path.join(CSRC, "gemm_x6_tile.h"), os.path.join(CSRC, "gemm_b16_tile.h"), os.path.join(os.path.dirname(HERE), "include", "k3m_hip.h")]
+    deps = [os.path.join(CSRC, "common.h"), os.path.join(CSRC, "gemm_f32_tile.h"), os.path.join(CSRC, "gemm_x6_tile.h"), os.path.join(CSRC, "gemm_b16_tile.h"), os.path.join(CSRC, "flash_frag.h"), os.path.join(os.path.dirname(HERE), "include", "k3m_hip.h")]
     dep_m = max(os.path.getmtime(d) for d in deps)
 
     def one(src):

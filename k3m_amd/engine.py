@@ -200,10 +200,9 @@ class FFN(object):
 
 
 def _flash(q, hd, lq, lk):
-    # bf16 encoder: the LSE-saving bf16 kernels (attention_bf16.hip, L <= 128); fp32 and longer
-    # sequences (or a 128 x 128 head-dim-128 co-attention whose backward images exceed the LDS): the
-    # exact-fp32 kernels (attention.hip, attention_long.hip), which also read/write bf16
-    return q.dtype == torch.bfloat16 and ops.flash_fits(lq, lk, hd)
+    # bf16 encoder: the LSE-saving bf16 kernels (attention_bf16.hip for whole heads of L <= 128,
+    # attention_flash_long.hip up to L = 512); fp32: the exact-fp32 kernels (attention.hip, attention_long.hip)
+    return q.dtype == torch.bfloat16 and (ops.flash_fits(lq, lk, hd) or ops.flash_long_fits(lq, lk, hd))
 
 
 def _attn_fwd(q, k, v, mask, nseq, lq, lk, nh, p, rng, out=None):

@@ -1,5 +1,6 @@
 """Tensor-level wrappers over the C ABI (k3m_amd/_lib.py).  Every function launches libk3m_hip
 kernels on torch's current stream; torch is used only to allocate outputs/workspaces."""
+import ctypes as C
 import os
 
 import torch
@@ -500,6 +501,15 @@ def flash_fits(lq, lk, hd):
     return max(fwd, bwd) <= LDS_MAX
 
 
+FLASH_LONG = os.environ.get("K3M_FLASH_LONG", "1") != "0"
+LONG_MAXL = 512   # max_position_embeddings (config/bert_base_6layer_6conect.json:8)
+
+
+def flash_long_fits(lq, lk, hd):
+    """attention_flash_long.hip: bf16 flash attention for any lq, lk <= 512 (the shapes flash_fits rejects)."""
+    return FLASH_LONG and 0 < lq <= LONG_MAXL and 0 < lk <= LONG_MAXL and hd in (64, 96, 128)
+
+
 def attn_fwd(q, k, v, kmask, ctx, probs, nseq, lq, lk, nh, hd, scale, p_drop, seed, off):
     name = "k3m_attn_fwd" if _short_fits(lq, lk, hd, False) else "k3m_attn_long_fwd"
     call(name, ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v), ptr(kmask), ptr(ctx), _ld(ctx), ptr(probs),
@@ -519,15 +529,37 @@ def attn_bwd(dctx, o, q, k, v, probs, dq, dk, dv, nseq, lq, lk, nh, hd, scale, p
 
 
 def flash_attn_fwd(q, k, v, kmask, ctx, lse, nseq, lq, lk, nh, hd, scale, p_drop, seed, off):
-    """bf16 attention forward saving the row log-sum-exp (lse: fp32 [nseq*nh*lq])."""
-    call("k3m_flash_attn_fwd", ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v), ptr(kmask), ptr(ctx), _ld(ctx),
+    """bf16 attention forward saving the row log-sum-exp (lse: fp32 [nseq*nh*lq]): the whole-head kernels of
+    attention_bf16.hip where they fit (L <= 128), else attention_flash_long.hip (L <= 512)."""
+    name = "k3m_flash_attn_fwd" if flash_fits(lq, lk, hd) else "k3m_flash_attn_long_fwd"
+    call(name, ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v), ptr(kmask), ptr(ctx), _ld(ctx),
          ptr(lse), nseq, lq, lk, nh, hd, scale, p_drop, seed, off, stream())
 
 
+_ws_cache = {}
+
+
+def flash_long_ws_bytes(nseq, lq, lk, nh, hd):
+    key = (nseq, lq, lk, nh, hd)
+    b = _ws_cache.get(key)
+    if b is None:
+        out = C.c_longlong(0)
+        call("k3m_flash_attn_long_ws_bytes", nseq, lq, lk, nh, hd, C.addressof(out))
+        b = _ws_cache[key] = int(out.value)
+    return b
+
+
 def flash_attn_bwd(dctx, o, q, k, v, kmask, lse, dq, dk, dv, nseq, lq, lk, nh, hd, scale, p_drop, seed, off):
-    call("k3m_flash_attn_bwd", ptr(dctx), _ld(dctx), ptr(o), _ld(o), ptr(q), _ld(q), ptr(k), _ld(k), ptr(v), _ld(v),
-         ptr(kmask), ptr(lse), ptr(dq), ptr(dk), ptr(dv), _ld(dq), _ld(dk), _ld(dv), nseq, lq, lk, nh, hd, scale,
-         p_drop, seed, off, stream())
+    if flash_fits(lq, lk, hd):
+        call("k3m_flash_attn_bwd", ptr(dctx), _ld(dctx), ptr(o), _ld(o), ptr(q), _ld(q), ptr(k), _ld(k), ptr(v),
+             _ld(v), ptr(kmask), ptr(lse), ptr(dq), ptr(dk), ptr(dv), _ld(dq), _ld(dk), _ld(dv), nseq, lq, lk, nh, hd,
+             scale, p_drop, seed, off, stream())
+        return
+    nb = flash_long_ws_bytes(nseq, lq, lk, nh, hd)
+    ws = torch.empty((max(nb, 16),), dtype=torch.uint8, device=dq.device)
+    call("k3m_flash_attn_long_bwd", ptr(dctx), _ld(dctx), ptr(o), _ld(o), ptr(q), _ld(q), ptr(k), _ld(k), ptr(v),
+         _ld(v), ptr(kmask), ptr(lse), ptr(dq), ptr(dk), ptr(dv), _ld(dq), _ld(dk), _ld(dv), ptr(ws), nb, nseq, lq, lk,
+         nh, hd, scale, p_drop, seed, off, stream())
 
 
 # ------------------------------------------------------------------ elementwise / rows

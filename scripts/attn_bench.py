@@ -21,6 +21,14 @@ SHAPES = [  # name, nseq, lq, lk, nh, hd
     ("co2 pv->txt", B, 128, 36, 8, 96),
     ("co2 txt->pv", B, 36, 128, 8, 96),
 ]
+# BASELINE configs[4] (bs=128, PV 320): the shapes attention_flash_long.hip serves in bf16
+SHAPES5 = [
+    ("pv self", 256, 320, 320, 12, 64),
+    ("co pv->img", 128, 320, 37, 8, 128),
+    ("co img->pv", 128, 37, 320, 8, 128),
+    ("co2 pv->txt", 128, 320, 36, 8, 96),
+    ("co2 txt->pv", 128, 36, 320, 8, 96),
+]
 
 
 def run(name, nseq, lq, lk, nh, hd, dtype, reps=20):
@@ -74,10 +82,11 @@ if __name__ == "__main__":
     L.load()
     dts = {"fp32": [torch.float32], "bf16": [torch.bfloat16], "both": [torch.float32, torch.bfloat16]}[
         sys.argv[1] if len(sys.argv) > 1 else "both"]
+    shapes = SHAPES5 if len(sys.argv) > 2 and sys.argv[2] == "cfg5" else SHAPES
     for d in dts:
-        for sh in SHAPES:
+        for sh in shapes:
             run(*sh, dtype=d)
     if torch.bfloat16 in dts:
         FLASH = False
-        for sh in SHAPES:
+        for sh in shapes:
             run(*sh, dtype=torch.bfloat16)

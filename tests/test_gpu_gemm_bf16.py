@@ -206,10 +206,16 @@ def test_attention_bf16(dev, lq, lk, nh, hd):
                                          (128, 37, 8, 128), (37, 128, 8, 128), (128, 36, 8, 128), (20, 90, 4, 64),
                                          (128, 36, 8, 96), (36, 128, 8, 96),
                                          (1, 5, 2, 64), (128, 101, 8, 128), (128, 128, 8, 128), (96, 128, 12, 64),
-                                         (65, 128, 4, 64), (128, 128, 8, 96), (33, 64, 3, 64)])
+                                         (65, 128, 4, 64), (128, 128, 8, 96), (33, 64, 3, 64),
+                                         # L > 128: attention_flash_long.hip (the config-5 shapes
+                                         # PV 320 self-attention, PV <-> title d = 96, PV <-> image d = 128), ragged
+                                         # and multi-key-group heads, the 512 maximum, a single query
+                                         (320, 320, 12, 64), (36, 320, 8, 96), (320, 36, 8, 96), (320, 37, 8, 128),
+                                         (37, 320, 8, 128), (512, 512, 2, 64), (200, 450, 3, 128), (450, 200, 2, 96),
+                                         (129, 129, 4, 64), (1, 300, 2, 64), (300, 7, 2, 128), (256, 50, 12, 64)])
 def test_flash_attention_bf16(dev, lq, lk, nh, hd):
-    """LSE-saving bf16 attention (attention_bf16.hip) against fp32 math on the same bf16 inputs,
-    and, with dropout on, against the probability-saving kernel drawing the same mask."""
+    """LSE-saving bf16 attention (attention_bf16.hip; attention_flash_long.hip past 128) against fp32 math on the
+    same bf16 inputs, and, with dropout on, against the probability-saving kernel drawing the same mask."""
     import math
     from k3m_amd import ops
     B, D = 5, nh * hd
@@ -254,3 +260,31 @@ def test_flash_attention_bf16(dev, lq, lk, nh, hd):
     ops.attn_bwd(dctx, c2, q, k, v, probs, *g2, B, lq, lk, nh, hd, sc, 0.1, 11, 5)
     for a, b in zip(g1, g2):
         assert _rel(a, b) < 4e-2
+
+
+@pytest.mark.parametrize("lq,lk,nh,hd", [(320, 320, 4, 64), (37, 320, 8, 128), (100, 512, 2, 96)])
+def test_flash_long_backward_deterministic(dev, lq, lk, nh, hd):
+    """attention_flash_long.hip's backward has no atomics: heads split into key groups reduce their fp32 dQ partials
+    in group order, so two runs are bit-identical (dropout on)."""
+    import math
+    from k3m_amd import ops
+    B, D = 3, nh * hd
+    g = torch.Generator(device="cpu").manual_seed(7)
+    q = torch.randn(B * lq, D, generator=g).to(dev).bfloat16()
+    k = torch.randn(B * lk, D, generator=g).to(dev).bfloat16()
+    v = torch.randn(B * lk, D, generator=g).to(dev).bfloat16()
+    mask = torch.zeros(B, lk, device=dev)
+    mask[:, lk - 5:] = -10000.0
+    ctx = torch.empty(B * lq, D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * nh * lq, device=dev)
+    sc = 1 / math.sqrt(hd)
+    ops.flash_attn_fwd(q, k, v, mask, ctx, lse, B, lq, lk, nh, hd, sc, 0.1, 3, 17)
+    dctx = torch.randn(B * lq, D, generator=g).to(dev).bfloat16()
+    outs = []
+    for _ in range(2):
+        gr = [torch.full((B * n_, D), float("nan"), device=dev, dtype=torch.bfloat16) for n_ in (lq, lk, lk)]
+        ops.flash_attn_bwd(dctx, ctx, q, k, v, mask, lse, *gr, B, lq, lk, nh, hd, sc, 0.1, 3, 17)
+        outs.append(gr)
+    for a, b in zip(*outs):
+        assert torch.isfinite(a.float()).all()
+        assert torch.equal(a, b)
