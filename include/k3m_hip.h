@@ -282,6 +282,24 @@ int k3m_sa_gather_bwd(const float* dX, const int64_t* index_p, const int64_t* in
                       void* dseq, float* dc_init, int batch, int len, int npv, int hidden, int dtype,
                       hipStream_t stream);
 
+/* Deterministic mode (K3M_DETERMINISTIC=1 in k3m_amd): the backward kernels above whose sums went through
+ * float atomics (order-dependent rounding: two runs of one step differed in the last bits), restated with every sum
+ * in a fixed order -- one owning workgroup per destination row, batch-wide sums through per-item partials reduced
+ * in item order.  Same arguments; the embedding form takes ws = [len][2][hidden] floats (type_vocab_size 2,
+ * config/bert_base_6layer_6conect.json) and the structure-attention form ws = [batch][hidden + 1] floats.
+ * hidden <= 1024 (embedding) / 2048 (structure aggregator). */
+int k3m_embed_bwd_det(const int64_t* ids, const int64_t* tt, const void* ds, float* dword, float* dpos, float* dtype_,
+                      int nseq, int len, int hidden, float* ws, int dtype, hipStream_t stream);
+int k3m_sa_attn_bwd_det(const float* dagg, const float* T, const float* att, const int32_t* nvalid,
+                        const int32_t* src, const float* w2, float* dT, float* dw2, float* db2, float* dc_init,
+                        float* ws, int batch, int npv, int hidden, hipStream_t stream);
+int k3m_lpm_bwd_det(const float* c_final, const float* X, const int32_t* nvalid, const int64_t* ent_neg,
+                    const int64_t* val_neg, int batch, int npv, int hidden, int n_ent, int n_val, const float* ws,
+                    float* dc_final, float* dX, hipStream_t stream);
+int k3m_sa_gather_bwd_det(const float* dX, const int64_t* index_p, const int64_t* index_v, const int32_t* nvalid,
+                          void* dseq, float* dc_init, int batch, int len, int npv, int hidden, int dtype,
+                          hipStream_t stream);
+
 /* pytorch_transformers 1.1.0 AdamW (train_concap_struc.py:436-441) over a contiguous segment of
  * the flat parameter buffer: m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
  * p -= lr*sqrt(1-b2^t)/(1-b1^t) * m/(sqrt(v)+eps); p -= lr*wd*p.  Optionally writes a bf16 copy

@@ -81,6 +81,10 @@ SIGNATURES = {
     "k3m_lpm_bwd": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, f32, vp, vp, vp, vp],
     "k3m_lpm_sample": [vp, i32, i32, i32, i32, u64, u64, vp, vp, vp],
     "k3m_sa_gather_bwd": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
+    "k3m_embed_bwd_det": [vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, i32, vp],
+    "k3m_sa_attn_bwd_det": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp],
+    "k3m_lpm_bwd_det": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp],
+    "k3m_sa_gather_bwd_det": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
     "k3m_adamw": [vp, vp, vp, vp, vp, i64, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double, i32, f32, vp],
     "k3m_adamw_ex": [vp, vp, vp, vp, vp, i64, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double, i32, f32,
                      i32, vp],

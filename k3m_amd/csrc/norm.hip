@@ -642,6 +642,80 @@ __global__ __launch_bounds__(256) void embed_bwd_pos_type_kernel(const int64_t* 
   atomicAdd(dtyp + cols + c, s1);
 }
 
+// Deterministic mode (k3m_embed_bwd_det, K3M_DETERMINISTIC): the same gradients with every sum in a fixed
+// order.  Word rows: one wave per token row; the wave of the FIRST row holding an id owns it and sums the
+// rows of every occurrence of that id in row order, then adds the total to dword[id] (one owner, plain
+// read-modify-write).  A wave finds whether its row is a first occurrence with one 64-wide ballot per 64
+// earlier ids.
+template <typename T, int CPL>
+__global__ __launch_bounds__(256) void embed_bwd_det_kernel(const int64_t* __restrict__ ids, const T* __restrict__ ds,
+                                                            float* __restrict__ dword, int rows, int cols) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const long long id = ids[row];
+  if (id == 0) return;   // padding_idx = 0 (vilbert_k3m.py:344)
+  for (int r0 = 0; r0 < row; r0 += 64) {
+    const int r = r0 + lane;
+    const bool same = r < row && ids[r] == id;
+    if (__ballot(same) != 0ull) return;   // an earlier row owns this id
+  }
+  float acc[CPL];
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) acc[q] = 0.f;
+  for (int r0 = row; r0 < rows; r0 += 64) {
+    const int r = r0 + lane;
+    unsigned long long m = __ballot(r < rows && ids[r] == id);
+    while (m) {   // matches in row order
+      const int rr = r0 + __builtin_ctzll(m);
+      m &= m - 1;
+      const T* src = ds + (long long)rr * cols;
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) {
+        const int c = lane + 64 * q;
+        if (c < cols) acc[q] += to_f(src[c]);
+      }
+    }
+  }
+  float* dst = dword + id * cols;
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    const int c = lane + 64 * q;
+    if (c < cols) dst[c] += acc[q];
+  }
+}
+
+// positions as embed_bwd_pos_type_kernel (one owner per (position, column)); the token-type sums of each
+// position go to ws[l][t][c] and embed_type_reduce_kernel adds them up over the positions in order
+template <typename T>
+__global__ __launch_bounds__(256) void embed_bwd_pos_type_det_kernel(const int64_t* __restrict__ tt,
+                                                                     const T* __restrict__ ds, float* dpos, float* ws,
+                                                                     int nseq, int len, int cols) {
+  const int l = blockIdx.x;
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float sp = 0.f, s0 = 0.f, s1 = 0.f;
+  for (int s = 0; s < nseq; ++s) {
+    const long long row = (long long)s * len + l;
+    const float g = to_f(ds[row * cols + c]);
+    sp += g;
+    if (tt[row] == 0) s0 += g;
+    else s1 += g;   // type_vocab_size 2 (checked on the host side of k3m_embed_bwd_det)
+  }
+  dpos[(long long)l * cols + c] += sp;
+  ws[((long long)l * 2) * cols + c] = s0;
+  ws[((long long)l * 2 + 1) * cols + c] = s1;
+}
+__global__ __launch_bounds__(256) void embed_type_reduce_kernel(const float* __restrict__ ws, float* dtyp, int len,
+                                                                int cols) {
+  const int i = blockIdx.x * 256 + threadIdx.x;   // (type, column)
+  if (i >= 2 * cols) return;
+  const int t = i / cols, c = i % cols;
+  float a = 0.f;
+  for (int l = 0; l < len; ++l) a += ws[((long long)l * 2 + t) * cols + c];
+  dtyp[(long long)t * cols + c] += a;
+}
+
 // ------------------------------------------------------------------ column sums
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, long long ld, int rows, int cols,
@@ -935,6 +1009,27 @@ extern "C" int k3m_embed_bwd(const int64_t* ids, const int64_t* tt, const void* 
   K3M_CHECK_LAUNCH();
   DISPATCH_T(dtype, hipLaunchKernelGGL(embed_bwd_pos_type_kernel<T>, dim3(len, k3m_cdiv(hidden, 256)), dim3(256), 0, st,
                                        tt, (const T*)ds, dpos, dtype_, nseq, len, hidden));
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_embed_bwd_det(const int64_t* ids, const int64_t* tt, const void* ds, float* dword, float* dpos,
+                                 float* dtype_, int nseq, int len, int hidden, float* ws, int dtype, hipStream_t st) {
+  K3M_ARG(ids && tt && ds && dword && dpos && dtype_ && ws && hidden <= 1024);
+  const int rows = nseq * len;
+  if (rows == 0) return 0;
+  if (hidden <= 768) {
+    DISPATCH_T(dtype, hipLaunchKernelGGL((embed_bwd_det_kernel<T, 12>), dim3(k3m_cdiv(rows, 4)), dim3(256), 0, st, ids,
+                                         (const T*)ds, dword, rows, hidden));
+  } else {
+    DISPATCH_T(dtype, hipLaunchKernelGGL((embed_bwd_det_kernel<T, 16>), dim3(k3m_cdiv(rows, 4)), dim3(256), 0, st, ids,
+                                         (const T*)ds, dword, rows, hidden));
+  }
+  K3M_CHECK_LAUNCH();
+  DISPATCH_T(dtype, hipLaunchKernelGGL(embed_bwd_pos_type_det_kernel<T>, dim3(len, k3m_cdiv(hidden, 256)), dim3(256), 0,
+                                       st, tt, (const T*)ds, dpos, ws, nseq, len, hidden));
+  hipLaunchKernelGGL(embed_type_reduce_kernel, dim3(k3m_cdiv(2 * hidden, 256)), dim3(256), 0, st, ws, dtype_, len,
+                     hidden);
   K3M_CHECK_LAUNCH();
   return 0;
 }

@@ -345,6 +345,218 @@ __global__ __launch_bounds__(NT) void sa_gather_bwd_kernel(const float* dX, cons
   }
 }
 
+// ---------------------------------------------------------------- deterministic mode (K3M_DETERMINISTIC)
+// The same backward with every sum in a fixed order (no float atomics): a destination row has one owning
+// workgroup, which adds its contributions in item / triple order; sums over the whole batch (dw2, db2) go
+// through per-item partials reduced in item order.
+
+constexpr int SA_CPT = 8;   // columns per thread (hidden <= 2048)
+
+// sa_attn_bwd_kernel's contribution of item i (triples of src s >= 0) to dT[s] (plain read-modify-write: the
+// caller owns s), to this thread's dw2 columns (acc) and to db (returned, thread 0)
+__device__ __forceinline__ float sa_item_bwd(const float* dagg, const float* T, const float* att, const float* w2, float* dT,
+                             int i, int s, int n, int npv, int h, float* acc, float* red, float* datt) {
+  const float* dg = dagg + (long long)i * h;
+  const float* at = att + (long long)i * npv;
+  for (int j = 0; j < n; ++j) {
+    const float* t = T + ((long long)s * npv + j) * h;
+    float a = 0.f;
+    for (int c = threadIdx.x; c < h; c += NT) a += dg[c] * t[c];
+    a = block_sum<4>(a, red);
+    if (threadIdx.x == 0) datt[j] = a;
+  }
+  __syncthreads();
+  float dot = 0.f;
+  for (int j = 0; j < n; ++j) dot += at[j] * datt[j];
+  float db = 0.f;
+  for (int j = 0; j < n; ++j) {
+    const float dbeta = at[j] * (datt[j] - dot);
+    db += dbeta;
+    const float* t = T + ((long long)s * npv + j) * h;
+    float* dt = dT + ((long long)s * npv + j) * h;
+#pragma unroll
+    for (int q = 0; q < SA_CPT; ++q) {
+      const int c = threadIdx.x + q * NT;
+      if (c >= h) break;
+      const float tv = t[c];
+      dt[c] += at[j] * dg[c] + dbeta * w2[c] * (tv > 0.f ? 1.f : 0.01f);
+      acc[q] += dbeta * lrelu(tv);
+    }
+  }
+  __syncthreads();   // datt is reused by the next item
+  return db;
+}
+
+// block b owns dT[b] (when item b has triples) and handles the items that read b's triples (b itself and the
+// zero-triple items after it: src is a running max, so they follow b contiguously); block 0 also adds the
+// leading zero-triple items (src = -1) to c_initial row 0.  Partial dw2 / db2 -> ws[b][0 .. h].
+__global__ __launch_bounds__(NT) void sa_attn_bwd_det_kernel(const float* dagg, const float* T, const float* att,
+                                                             const int32_t* nvalid, const int32_t* src,
+                                                             const float* w2, float* dT, float* dc_init, float* ws,
+                                                             int batch, int npv, int h) {
+  __shared__ float red[4];
+  __shared__ float datt[64];
+  const int b = blockIdx.x;
+  float acc[SA_CPT];
+#pragma unroll
+  for (int q = 0; q < SA_CPT; ++q) acc[q] = 0.f;
+  float db = 0.f;
+  if (b == 0) {
+    for (int i = 0; i < batch && src[i] < 0; ++i)
+      for (int c = threadIdx.x; c < h; c += NT) dc_init[c] += dagg[(long long)i * h + c];
+  }
+  const int n = nvalid[b];
+  if (n > 0)
+    for (int i = b; i < batch && src[i] == b; ++i) db += sa_item_bwd(dagg, T, att, w2, dT, i, b, n, npv, h, acc, red, datt);
+  float* wb = ws + (long long)b * (h + 1);
+#pragma unroll
+  for (int q = 0; q < SA_CPT; ++q)
+    if (threadIdx.x + q * NT < h) wb[threadIdx.x + q * NT] = acc[q];
+  if (threadIdx.x == 0) wb[h] = db;
+}
+__global__ __launch_bounds__(NT) void sa_w2_reduce_kernel(const float* ws, float* dw2, float* db2, int batch, int h) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c > h) return;
+  float a = 0.f;
+  for (int b = 0; b < batch; ++b) a += ws[(long long)b * (h + 1) + c];
+  if (c < h) dw2[c] += a;
+  else db2[0] += a;
+}
+
+// LPM backward, own-item part: block i walks its triples in order; its own X rows (p, v and the value
+// negatives, all rows of item i) and c_final[i] get plain read-modify-writes.  The entity negatives' terms
+// on other items' c_final rows are lpm_bwd_ent_det_kernel's.
+__global__ __launch_bounds__(NT) void lpm_bwd_item_det_kernel(const float* cf, const float* X, const int32_t* nvalid,
+                                                              const int64_t* ent, const int64_t* val, int npv, int h,
+                                                              int ke, int kv, const float* ws, int total, float* dcf,
+                                                              float* dX) {
+  const int K = ke + kv;
+  const int i = blockIdx.x;
+  const float* hinge = ws;
+  const float* posn = ws + (long long)total * K;
+  const float* negn = posn + total;
+  const float w = 1.f / ws[(long long)total * (2 * K + 1)];
+  float gci_acc[SA_CPT];
+#pragma unroll
+  for (int q = 0; q < SA_CPT; ++q) gci_acc[q] = 0.f;
+  const int n = nvalid[i];
+  for (int j = 0; j < n; ++j) {
+    const long long ij = (long long)i * npv + j;
+    const float* x = X + ij * 3 * h;
+    float* dx = dX + ij * 3 * h;
+    float cpos = 0.f;
+    float cneg[LPM_KMAX];
+    int kk[LPM_KMAX];
+#pragma unroll
+    for (int e = 0; e < LPM_KMAX; ++e) {
+      cneg[e] = 0.f;
+      kk[e] = -1;
+      int k;
+      if (e < K && pair_neg(ent, val, ij, e, ke, kv, k) && hinge[ij * K + e] > 0.f) {
+        cpos -= w;
+        cneg[e] = w / fmaxf(negn[ij * K + e], 1e-30f);
+        kk[e] = k;
+      }
+    }
+    const float cp = cpos / fmaxf(posn[ij], 1e-30f);
+#pragma unroll
+    for (int q = 0; q < SA_CPT; ++q) {
+      const int c = threadIdx.x + q * NT;
+      if (c >= h) break;
+      const float p = x[h + c], v = x[2 * h + c];
+      const float up = cf[(long long)i * h + c] + p - v;
+      float gci = cp * up, gp = cp * up, gv = -cp * up;
+#pragma unroll
+      for (int e = 0; e < LPM_KMAX; ++e) {
+        if (kk[e] < 0) continue;
+        if (e < ke) {
+          const float g = cneg[e] * (cf[(long long)kk[e] * h + c] + p - v);
+          gp += g;
+          gv -= g;
+        } else {
+          const long long ik = (long long)i * npv + kk[e];
+          const float g = cneg[e] * (cf[(long long)i * h + c] + p - X[ik * 3 * h + 2 * h + c]);
+          gci += g;
+          gp += g;
+          dX[ik * 3 * h + 2 * h + c] -= g;
+        }
+      }
+      gci_acc[q] += gci;
+      dx[h + c] += gp;
+      dx[2 * h + c] += gv;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < SA_CPT; ++q)
+    if (threadIdx.x + q * NT < h) dcf[(long long)i * h + threadIdx.x + q * NT] += gci_acc[q];
+}
+
+// entity-negative terms on c_final[k]: block k scans every triple (item, triple, negative order) for the
+// active pairs whose entity negative is k
+__global__ __launch_bounds__(NT) void lpm_bwd_ent_det_kernel(const float* cf, const float* X, const int32_t* nvalid,
+                                                             const int64_t* ent, int batch, int npv, int h, int ke,
+                                                             int kv, const float* ws, int total, float* dcf) {
+  const int K = ke + kv;
+  const int k = blockIdx.x;
+  const float* hinge = ws;
+  const float* negn = ws + (long long)total * K + total;
+  const float w = 1.f / ws[(long long)total * (2 * K + 1)];
+  float acc[SA_CPT];
+#pragma unroll
+  for (int q = 0; q < SA_CPT; ++q) acc[q] = 0.f;
+  for (int i = 0; i < batch; ++i) {
+    const int n = nvalid[i];
+    for (int j = 0; j < n; ++j) {
+      const long long ij = (long long)i * npv + j;
+      for (int e = 0; e < ke; ++e) {
+        if (ent[ij * ke + e] != k || !(hinge[ij * K + e] > 0.f)) continue;
+        const float cn = w / fmaxf(negn[ij * K + e], 1e-30f);
+        const float* x = X + ij * 3 * h;
+#pragma unroll
+        for (int q = 0; q < SA_CPT; ++q) {
+          const int c = threadIdx.x + q * NT;
+          if (c < h) acc[q] += cn * (cf[(long long)k * h + c] + x[h + c] - x[2 * h + c]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < SA_CPT; ++q)
+    if (threadIdx.x + q * NT < h) dcf[(long long)k * h + threadIdx.x + q * NT] += acc[q];
+}
+
+// sa_gather_bwd_kernel with one workgroup per item walking its triples in order (every row it writes -- the
+// item's sequence rows and c_initial[i] -- belongs to that item)
+__global__ __launch_bounds__(NT) void sa_gather_bwd_det_kernel(const float* dX, const int64_t* index_p,
+                                                               const int64_t* index_v, const int32_t* nvalid,
+                                                               float* dseq, float* dc_init, int len, int npv, int h) {
+  const int i = blockIdx.x;
+  const int n = nvalid[i];
+  float* ds = dseq + (long long)i * len * h;
+  float acc[SA_CPT];
+#pragma unroll
+  for (int q = 0; q < SA_CPT; ++q) acc[q] = 0.f;
+  for (int j = 0; j < n; ++j) {
+    const long long ip = ((long long)i * npv + j) * 2;
+    const long long pa = index_p[ip], pb = index_p[ip + 1], va = index_v[ip], vb = index_v[ip + 1];
+    const float* dx = dX + ((long long)i * npv + j) * 3 * h;
+#pragma unroll
+    for (int q = 0; q < SA_CPT; ++q) {
+      const int c = threadIdx.x + q * NT;
+      if (c >= h) break;
+      acc[q] += dx[c];
+      const float gp = 0.5f * dx[h + c], gv = 0.5f * dx[2 * h + c];
+      ds[pa * h + c] += gp;
+      ds[pb * h + c] += gp;
+      ds[va * h + c] += gv;
+      ds[vb * h + c] += gv;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < SA_CPT; ++q)
+    if (threadIdx.x + q * NT < h) dc_init[(long long)i * h + threadIdx.x + q * NT] += acc[q];
+}
+
 }  // namespace
 
 extern "C" int k3m_sa_gather(const void* seq, const int64_t* index_p, const int64_t* index_v, const float* c_init,
@@ -429,6 +641,48 @@ extern "C" int k3m_sa_gather_bwd(const float* dX, const int64_t* index_p, const 
   K3M_ARG(dtype == K3M_F32);
   if (batch == 0) return 0;
   hipLaunchKernelGGL(sa_gather_bwd_kernel<float>, dim3(batch * npv), dim3(NT), 0, st, dX, index_p, index_v, nvalid,
+                     (float*)dseq, dc_init, len, npv, hidden);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------- deterministic-mode entry points
+extern "C" int k3m_sa_attn_bwd_det(const float* dagg, const float* T, const float* att, const int32_t* nvalid,
+                                   const int32_t* src, const float* w2, float* dT, float* dw2, float* db2,
+                                   float* dc_init, float* ws, int batch, int npv, int hidden, hipStream_t st) {
+  K3M_ARG(dagg && T && att && nvalid && src && w2 && dT && dw2 && db2 && dc_init && ws && npv <= 64);
+  K3M_ARG(hidden <= SA_CPT * NT);
+  if (batch == 0) return 0;
+  hipLaunchKernelGGL(sa_attn_bwd_det_kernel, dim3(batch), dim3(NT), 0, st, dagg, T, att, nvalid, src, w2, dT, dc_init,
+                     ws, batch, npv, hidden);
+  hipLaunchKernelGGL(sa_w2_reduce_kernel, dim3(k3m_cdiv(hidden + 1, NT)), dim3(NT), 0, st, ws, dw2, db2, batch, hidden);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_lpm_bwd_det(const float* c_final, const float* X, const int32_t* nvalid, const int64_t* ent_neg,
+                               const int64_t* val_neg, int batch, int npv, int hidden, int n_ent, int n_val,
+                               const float* ws, float* dc_final, float* dX, hipStream_t st) {
+  K3M_ARG(c_final && X && nvalid && ws && dc_final && dX && n_ent >= 0 && n_val >= 0 && n_ent + n_val <= LPM_KMAX);
+  K3M_ARG((ent_neg || n_ent == 0) && (val_neg || n_val == 0) && hidden <= SA_CPT * NT);
+  const int total = batch * npv;
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(lpm_bwd_item_det_kernel, dim3(batch), dim3(NT), 0, st, c_final, X, nvalid, ent_neg, val_neg, npv,
+                     hidden, n_ent, n_val, ws, total, dc_final, dX);
+  if (n_ent > 0)
+    hipLaunchKernelGGL(lpm_bwd_ent_det_kernel, dim3(batch), dim3(NT), 0, st, c_final, X, nvalid, ent_neg, batch, npv,
+                       hidden, n_ent, n_val, ws, total, dc_final);
+  K3M_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int k3m_sa_gather_bwd_det(const float* dX, const int64_t* index_p, const int64_t* index_v,
+                                     const int32_t* nvalid, void* dseq, float* dc_init, int batch, int len, int npv,
+                                     int hidden, int dtype, hipStream_t st) {
+  K3M_ARG(dX && index_p && index_v && nvalid && dseq && dc_init && hidden <= SA_CPT * NT);
+  K3M_ARG(dtype == K3M_F32);
+  if (batch == 0) return 0;
+  hipLaunchKernelGGL(sa_gather_bwd_det_kernel, dim3(batch), dim3(NT), 0, st, dX, index_p, index_v, nvalid,
                      (float*)dseq, dc_init, len, npv, hidden);
   K3M_CHECK_LAUNCH();
   return 0;

@@ -1012,10 +1012,16 @@ class K3MEngine(object):
          margin) = ctx["struct"]
         dcf = torch.zeros_like(c_final)
         dX = torch.zeros_like(X)
+        det = ops.DETERMINISTIC   # fixed-order forms of the three kernels below (no float atomics)
         if lws is not None:
-            L.call("k3m_lpm_bwd", c_final.data_ptr(), X.data_ptr(), nvalid.data_ptr(), L.ptr(ent_neg), L.ptr(val_neg), B,
-                   NPV, H, ent_neg.shape[2], val_neg.shape[2], margin, lws.data_ptr(), dcf.data_ptr(), dX.data_ptr(),
-                   L.stream())
+            if det:
+                L.call("k3m_lpm_bwd_det", c_final.data_ptr(), X.data_ptr(), nvalid.data_ptr(), L.ptr(ent_neg),
+                       L.ptr(val_neg), B, NPV, H, ent_neg.shape[2], val_neg.shape[2], lws.data_ptr(), dcf.data_ptr(),
+                       dX.data_ptr(), L.stream())
+            else:
+                L.call("k3m_lpm_bwd", c_final.data_ptr(), X.data_ptr(), nvalid.data_ptr(), L.ptr(ent_neg),
+                       L.ptr(val_neg), B, NPV, H, ent_neg.shape[2], val_neg.shape[2], margin, lws.data_ptr(),
+                       dcf.data_ptr(), dX.data_ptr(), L.stream())
             if w_lpm != 1.0:
                 ops.add_(dcf, dcf.clone(), w_lpm - 1.0)
                 ops.add_(dX, dX.clone(), w_lpm - 1.0)
@@ -1029,16 +1035,24 @@ class K3MEngine(object):
         dT = torch.zeros_like(Tm)
         groups = ctx.get("groups", 1)
         Bg = B // groups
+        sa_ws = torch.empty((Bg * (H + 1),), dtype=torch.float32, device=dev) if det else None
         for gi in range(groups):
             r0 = gi * Bg
-            L.call("k3m_sa_attn_bwd", dagg[r0:].data_ptr(), Tm[r0 * NPV:].data_ptr(), att[r0:].data_ptr(),
-                   nvalid[r0:].data_ptr(), src[r0:].data_ptr(), fp.p["struc_w2.weight"].data_ptr(),
-                   dT[r0 * NPV:].data_ptr(), fp.g["struc_w2.weight"].data_ptr(), fp.g["struc_w2.bias"].data_ptr(),
-                   dci[r0:].data_ptr(), Bg, NPV, H, L.stream())
+            if det:
+                L.call("k3m_sa_attn_bwd_det", dagg[r0:].data_ptr(), Tm[r0 * NPV:].data_ptr(), att[r0:].data_ptr(),
+                       nvalid[r0:].data_ptr(), src[r0:].data_ptr(), fp.p["struc_w2.weight"].data_ptr(),
+                       dT[r0 * NPV:].data_ptr(), fp.g["struc_w2.weight"].data_ptr(), fp.g["struc_w2.bias"].data_ptr(),
+                       dci[r0:].data_ptr(), sa_ws.data_ptr(), Bg, NPV, H, L.stream())
+            else:
+                L.call("k3m_sa_attn_bwd", dagg[r0:].data_ptr(), Tm[r0 * NPV:].data_ptr(), att[r0:].data_ptr(),
+                       nvalid[r0:].data_ptr(), src[r0:].data_ptr(), fp.p["struc_w2.weight"].data_ptr(),
+                       dT[r0 * NPV:].data_ptr(), fp.g["struc_w2.weight"].data_ptr(), fp.g["struc_w2.bias"].data_ptr(),
+                       dci[r0:].data_ptr(), Bg, NPV, H, L.stream())
         self.sw1.wgrad(dT, X)
         self.sw1.dgrad(dT, dx=dX, beta=1.0)
-        L.call("k3m_sa_gather_bwd", dX.data_ptr(), index_p.data_ptr(), index_v.data_ptr(), nvalid.data_ptr(),
-               dseq_tp[BT:].data_ptr(), dci.data_ptr(), B, P, NPV, H, L.F32, L.stream())
+        L.call("k3m_sa_gather_bwd_det" if det else "k3m_sa_gather_bwd", dX.data_ptr(), index_p.data_ptr(),
+               index_v.data_ptr(), nvalid.data_ptr(), dseq_tp[BT:].data_ptr(), dci.data_ptr(), B, P, NPV, H, L.F32,
+               L.stream())
 
         # ---- pooled outputs
         (mean_v,) = ctx["pool"]

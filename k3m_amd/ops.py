@@ -454,8 +454,25 @@ def embed_fwd(ids, tt, word, pos, typ, gamma, beta, y0, y1, y2, xhat, rstd, p_ou
          ptr(y2), ptr(xhat), ptr(rstd), nseq, ln, word.shape[1], eps, p_out, seed, off, dt(y0), stream())
 
 
+# Deterministic mode (SURVEY §5 "deterministic-mode flag"): the backward kernels that summed through float atomics
+# (embedding rows, structure aggregator, LPM) run their fixed-order forms (k3m_*_det), so a step is bit-reproducible
+# run to run.  K3M_DETERMINISTIC=1 at import, or set_deterministic() at run time.
+DETERMINISTIC = os.environ.get("K3M_DETERMINISTIC", "0") not in ("", "0")
+
+
+def set_deterministic(on=True):
+    global DETERMINISTIC
+    DETERMINISTIC = bool(on)
+
+
 def embed_bwd(ids, tt, ds, dword, dpos, dtyp):
     nseq, ln = ids.shape
+    if DETERMINISTIC:
+        assert dtyp.shape[0] == 2, "deterministic embedding backward: type_vocab_size 2"
+        ws = torch.empty((ln * 2 * dword.shape[1],), dtype=torch.float32, device=ds.device)
+        call("k3m_embed_bwd_det", ptr(ids), ptr(tt), ptr(ds), ptr(dword), ptr(dpos), ptr(dtyp), nseq, ln,
+             dword.shape[1], ptr(ws), dt(ds), stream())
+        return
     call("k3m_embed_bwd", ptr(ids), ptr(tt), ptr(ds), ptr(dword), ptr(dpos), ptr(dtyp), nseq, ln, dword.shape[1],
          dt(ds), stream())
 
