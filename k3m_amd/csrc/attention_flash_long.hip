@@ -197,29 +197,34 @@ __global__ __launch_bounds__(FNT, 2) void flash_long_fwd_kernel(const uint16_t* 
 }
 
 // ------------------------------------------------------------------ backward
-// D[(s nh + h) lq + i] = dO_i . O_i over the head's dims (the bf16 O the forward wrote)
+// D[(s nh + h) lq + i] = dO_i . O_i over the head's dims (the bf16 O the forward wrote): 16 lanes per (row, head),
+// lane c loading the head's 16-B chunk c (hd / 8 <= 16 chunks), so a wave's loads are 4 whole head rows
 __global__ __launch_bounds__(256) void flash_long_prep_kernel(const uint16_t* __restrict__ dctx, long long ldc,
                                                               const uint16_t* __restrict__ o, long long ldo,
                                                               float* __restrict__ dvec, int nseq, int lq, int nh,
                                                               int hd) {
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long long)nseq * lq * nh) return;
-  const int h = (int)(idx % nh);
-  const long long row = idx / nh;   // sequence row s lq + i
-  const int s = (int)(row / lq), i = (int)(row % lq);
-  const uint16_t* pd = dctx + row * ldc + (long long)h * hd;
-  const uint16_t* po = o + row * ldo + (long long)h * hd;
+  const long long idx = ((long long)blockIdx.x * 256 + threadIdx.x) >> 4;   // (row, head)
+  const int c = threadIdx.x & 15;
+  const bool live = idx < (long long)nseq * lq * nh;
+  const long long id = live ? idx : 0;
+  const int h = (int)(id % nh);
+  const long long row = id / nh;   // sequence row s lq + i
   float acc = 0.f;
-  for (int c = 0; c < hd / 8; ++c) {
-    const uint4 a = *reinterpret_cast<const uint4*>(pd + 8 * c);
-    const uint4 b = *reinterpret_cast<const uint4*>(po + 8 * c);
+  if (live && c < hd / 8) {
+    const uint4 a = *reinterpret_cast<const uint4*>(dctx + row * ldc + (long long)h * hd + 8 * c);
+    const uint4 b = *reinterpret_cast<const uint4*>(o + row * ldo + (long long)h * hd + 8 * c);
     const uint32_t wa[4] = {a.x, a.y, a.z, a.w}, wb[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
     for (int t = 0; t < 4; ++t)
       acc += __uint_as_float(wa[t] << 16) * __uint_as_float(wb[t] << 16) +
              __uint_as_float(wa[t] & 0xffff0000u) * __uint_as_float(wb[t] & 0xffff0000u);
   }
-  dvec[((long long)s * nh + h) * lq + i] = acc;
+#pragma unroll
+  for (int m = 8; m > 0; m >>= 1) acc += __shfl_xor(acc, m, 64);
+  if (live && c == 0) {
+    const int s = (int)(row / lq), i = (int)(row % lq);
+    dvec[((long long)s * nh + h) * lq + i] = acc;
+  }
 }
 
 // waves per backward workgroup (key tiles of 32): 12 at d = 64 (3 waves per SIMD, 131 KB of LDS), 7 at
@@ -567,7 +572,7 @@ extern "C" int k3m_flash_attn_long_bwd(const void* dctx, long long ldc, const vo
   const long long rows = (long long)nseq * nh * lq;
   float* dvec = static_cast<float*>(ws);
   float* dq_ws = dvec + (rows + 63) / 64 * 64;
-  hipLaunchKernelGGL(flash_long_prep_kernel, dim3(k3m_cdiv(rows, 256)), dim3(256), 0, st, (const uint16_t*)dctx, ldc,
+  hipLaunchKernelGGL(flash_long_prep_kernel, dim3(k3m_cdiv(rows * 16, 256)), dim3(256), 0, st, (const uint16_t*)dctx, ldc,
                      (const uint16_t*)o, ldo, dvec, nseq, lq, nh, hd);
   const dim3 grid(nseq * nh, ngrp);
 #define K3M_FL_BWD(HD_)                                                                                          \

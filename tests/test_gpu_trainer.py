@@ -363,7 +363,8 @@ def test_deterministic_gradients_match_atomic_form(dev):
     for name, shape in fp.spec:
         o, n = fp.offsets[name], math.prod(shape)
         x, y = grads[0][o:o + n], grads[1][o:o + n]
-        tol = 1e-5 * float(x.abs().max()) + 1e-8   # key biases: gradient zero up to rounding
+        # key biases and struc_w2.bias: gradients that are zero up to rounding (a softmax gradient sums to 0)
+        tol = 1e-5 * float(x.abs().max()) + 1e-7
         if float((x - y).abs().max()) > tol:
             bad.append((name, float((x - y).abs().max()), tol))
     assert not bad, bad[:10]
