@@ -172,6 +172,65 @@ class CoattnProbe(object):
         return sum(s.elapsed_time(e) for s, e in self.events)
 
 
+class GemmAllProbe(object):
+    """HIP events around EVERY GEMM launch (single and grouped, as scripts/gemm_calls.py) of one eager step run after
+    the timed region: the step's GEMM aggregate (algorithmic TFLOP / GEMM ms) and its largest call class."""
+
+    def __init__(self):
+        self.rec = []
+        self.active = False
+
+    def install(self):
+        import torch
+        from k3m_amd import ops, _lib as L
+        orig = L.call
+        probe = self
+
+        def sig(g):
+            return "%s%s m=%d n=%d k=%d epi=%d s=%d" % ("t" if g.a_trans else "n", "t" if g.b_trans else "n", g.m, g.n,
+                                                        g.k, g.epilogue & 0xff, g.splitk)
+
+        def wrapped(name, *a):
+            if not probe.active or name not in ("k3m_gemm", "k3m_gemm_grouped"):
+                return orig(name, *a)
+            if name == "k3m_gemm":
+                gs = [a[0]._obj]
+            else:
+                arr = L.C.cast(a[0], L.C.POINTER(L.K3mGemm))
+                gs = [arr[i] for i in range(a[1])]
+            key = ("group[%d] " % len(gs) if name == "k3m_gemm_grouped" else "") + " + ".join(sig(g) for g in gs)
+            flops = sum(2.0 * g.m * g.n * g.k for g in gs)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            r = orig(name, *a)
+            e.record()
+            probe.rec.append((key, flops, s, e))
+            return r
+        L.call = wrapped
+        ops.call = wrapped
+
+    def summary(self, peak):
+        import collections
+        agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
+        for key, flops, s, e in self.rec:
+            a = agg[key]
+            a[0] += 1
+            a[1] += s.elapsed_time(e)
+            a[2] += flops
+        ms = sum(v[1] for v in agg.values())
+        tf = sum(v[2] for v in agg.values()) / 1e12
+        if ms <= 0:
+            return None
+        top_key, (n, tms, tfl) = max(agg.items(), key=lambda kv: kv[1][1])
+        return {"ms_per_step": round(ms, 3), "tflop_per_step": round(tf, 4), "launches": len(self.rec),
+                "achieved": round(tf / (ms * 1e-3), 2), "peak": peak / 1e12, "unit": "TFLOP/s",
+                "frac": round(tf * 1e12 / (ms * 1e-3) / peak, 4),
+                "largest_class": {"calls": top_key[:160], "launches": n, "ms_per_step": round(tms, 3),
+                                  "share": round(tms / ms, 4), "achieved": round(tfl / (tms * 1e-3) / 1e12, 2)},
+                "probe": "HIP events around every GEMM launch of one eager step after the timed region "
+                         "(scripts/gemm_calls.py's method)"}
+
+
 def head_kernel(bf):
     """Full-name fragment of the kernel the probed GEMM runs at HEAD with the default knobs (gemm.hip /
     gemm_bf16.hip dispatch of a 256x256-tile problem of >= K3M_*_PERSIST_MIN blocks)."""
@@ -292,7 +351,10 @@ def cpu_baseline(cfg, shape, bsz, steps):
             "bs8_samples_s": round(8 * 2 / dt8, 4),
             "sample": "oracle/k3m_oracle.py fwd+bwd+AdamW, fp32, bs=%d, %d timed step(s) (%.1f s) after a bs=8 warm-up; "
                       "bs=8: 2 timed steps %.1f s (same shapes as the GPU workload; torch CPU, %d threads = this "
-                      "process's CPU share; the machine has %d)" % (bsz, steps, dt, dt8, ncores, os.cpu_count() or 0)}
+                      "process's CPU share; the machine has %d).  Bounded sample: the bench contract asks for ~10-30 s "
+                      "of CPU work so the default run ends in minutes, so bs=64 runs %d step(s), not SURVEY §8(d)'s 3 "
+                      "after 1 warm-up (--cpu-steps 3 runs those)" % (bsz, steps, dt, dt8, ncores, os.cpu_count() or 0,
+                                                                       steps)}
 
 
 def main():
@@ -344,6 +406,8 @@ def main():
     probe.install()
     cprobe = CoattnProbe()
     cprobe.install()
+    gall = GemmAllProbe()
+    gall.install()
 
     def barrier():
         if use_dist:
@@ -397,6 +461,13 @@ def main():
         barrier()
         probe.active = cprobe.active = False
         tr.graph = mode
+    # every GEMM of one eager step, after the timed region (the per-launch events would perturb the timed steps)
+    mode, tr.graph = tr.graph, False
+    gall.active = True
+    tr.step(batch)
+    barrier()
+    gall.active = False
+    tr.graph = mode
     tr.finish()
     ms_step = 1000.0 * dt / args.steps
     value = world * B * args.steps / dt
@@ -449,6 +520,7 @@ def main():
                      "peak_basis": ("bf16 dense MFMA" if bf else "fp32 via 6 bf16 MFMA partial products = bf16 dense "
                                     "peak / 6" if x6 else "f32 MFMA"),
                      "traffic_unit": "HBM bytes/launch (rocprofv3 PMC, %s)" % traffic_src if traffic else None},
+        "gemm_all": gall.summary(peak),
         "coattn": {"ms_per_step": round(co_ms, 3) if co_ms else None,
                    "algorithmic_tflop_per_step": round(co_flops / 1e12, 3),
                    "achieved": round(co_flops / (co_ms * 1e-3) / 1e12, 2) if co_ms else None,

@@ -24,17 +24,34 @@ namespace {
 
 using k3m_f32::gemm_f32_kernel;
 
+// C = epilogue(sum of the split-K slabs in slice order): the element formulas of the tile epilogues
+// (gemm_f32_tile.h epi_math), so a split problem ends exactly like the unsplit one would on its sums
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
                                                             float* __restrict__ C, long long ldc, float alpha,
-                                                            float beta) {
+                                                            float beta, int epi, const float* __restrict__ bias,
+                                                            float* __restrict__ aux, long long ldaux) {
   const long long total = (long long)M * N;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
     float s = 0.f;
     for (int k = 0; k < splits; ++k) s += ws[(long long)k * total + e];
     const int row = (int)(e / N), col = (int)(e % N);
     float* cp = C + (long long)row * ldc + col;
-    float o = alpha * s;
-    if (beta != 0.f) o += beta * *cp;
+    float o;
+    bool can_old = true;
+    switch (epi) {
+      case K3M_EPI_BIAS: o = alpha * (s + bias[col]); break;
+      case K3M_EPI_BIAS_GELU: {
+        const float pa = s + bias[col];
+        aux[(long long)row * ldaux + col] = pa;
+        o = gelu_f(pa);
+        can_old = false;
+        break;
+      }
+      case K3M_EPI_DGELU: o = alpha * s * dgelu_f(aux[(long long)row * ldaux + col]); break;
+      case K3M_EPI_BIAS_SIGMOID: o = sigmoid_f(s + bias[col]); can_old = false; break;
+      default: o = alpha * s;
+    }
+    if (can_old && beta != 0.f) o += beta * *cp;
     *cp = o;
   }
 }
@@ -175,6 +192,8 @@ int k3m_gemm_bf16_impl(const K3mGemm& g, hipStream_t st, bool slabs_only, bool c
 int k3m_gemm_bf16_grouped_impl(const K3mGemm* gs, int count, hipStream_t st, bool* handled, const bool* slabs_only);
 // (the grouped problems carry their COLSUM_SLABS request as a non-null ws with splitk <= 1)
 
+static int gemm_f32_dispatch(const K3mGemm& g, const K3mGemm& gr, int epi_out, bool slabs_only, hipStream_t st);
+
 extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
   if (!gp) return K3M_EINVAL;
   const bool slabs_only = (gp->epilogue & K3M_GEMM_SLABS_ONLY) != 0;
@@ -191,13 +210,83 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
   K3M_ARG(g.dtype == K3M_F32 || g.dtype == K3M_BF16);
   K3M_ARG(g.c_dtype == K3M_F32 || (g.dtype == K3M_BF16 && g.c_dtype == K3M_BF16));
   K3M_ARG(g.a && g.b && g.c);
-  K3M_ARG(g.splitk <= 1 || (g.epilogue == K3M_EPI_NONE && g.ws));
+  K3M_ARG(g.splitk <= 1 || ((g.epilogue == K3M_EPI_NONE || !slabs_only) && g.ws));
   K3M_ARG(g.epilogue == K3M_EPI_NONE || g.epilogue == K3M_EPI_DGELU || g.bias);
   K3M_ARG((g.epilogue != K3M_EPI_BIAS_GELU && g.epilogue != K3M_EPI_DGELU) || g.aux);
   K3M_ARG(g.f32_algo == K3M_F32_SPLIT_BF16X6 || g.f32_algo == K3M_F32_MFMA_F32);
   K3M_ARG(g.a_planes == 0 && g.b_planes == 0);   // reserved (the round-3 pre-split lab path, scripts/lab/r3)
   if (g.dtype == K3M_BF16) {
+    K3M_ARG(g.splitk <= 1 || g.epilogue == K3M_EPI_NONE);
     return k3m_gemm_bf16_impl(g, st, slabs_only, colsum);
+  }
+  // a split problem computes raw slabs (epilogue NONE); its epilogue runs in splitk_reduce_kernel
+  const int epi_out = g.epilogue;
+  K3mGemm gsplit = g;
+  if (g.splitk > 1) gsplit.epilogue = K3M_EPI_NONE;
+  return gemm_f32_dispatch(gsplit, g, epi_out, slabs_only, st);
+}
+
+namespace {
+// fp32 C[m, n] (n <= 8) = alpha A B + beta C for the skinny products of the step (the 5-column image-location
+// weight gradient, tn 1024 x 5 x 2,368): exact fp32 FMAs, 64 rows per workgroup, the k range dealt to the 16
+// waves in fixed interleaved order and reduced through LDS in wave order (deterministic).  The tile kernels
+// gave such a product 1-2 % of one CU's MFMA rate (64 us).
+constexpr int SKINNY_N = 8;
+constexpr int SKINNY_U = 8;   // k values per thread in flight
+__global__ __launch_bounds__(1024) void gemm_skinny_kernel(K3mGemm g) {
+  __shared__ float red[16][64][SKINNY_N + 1];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int m = blockIdx.x * 64 + lane;
+  const int mc = min(m, g.m - 1);   // clamped row: every lane loads, the store is masked
+  const float* A = static_cast<const float*>(g.a);
+  const float* B = static_cast<const float*>(g.b);
+  float acc[SKINNY_N];
+#pragma unroll
+  for (int j = 0; j < SKINNY_N; ++j) acc[j] = 0.f;
+  // wave w owns the contiguous k range [k0, k1); SKINNY_U loads of A issued before their FMAs
+  const int per = (g.k + 15) / 16, k0 = w * per, k1 = min(g.k, k0 + per);
+  for (int kb = k0; kb < k1; kb += SKINNY_U) {
+    float av[SKINNY_U];
+#pragma unroll
+    for (int u = 0; u < SKINNY_U; ++u) {
+      const int k = min(kb + u, k1 - 1);
+      const float x = g.a_trans ? A[(long long)k * g.lda + mc] : A[(long long)mc * g.lda + k];
+      av[u] = kb + u < k1 ? x : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < SKINNY_U; ++u) {
+      const int k = min(kb + u, k1 - 1);   // wave-uniform: B's row is a broadcast (scalar) load
+#pragma unroll
+      for (int j = 0; j < SKINNY_N; ++j)
+        if (j < g.n) acc[j] = fmaf(av[u], g.b_trans ? B[(long long)j * g.ldb + k] : B[(long long)k * g.ldb + j], acc[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < SKINNY_N; ++j) red[w][lane][j] = acc[j];
+  __syncthreads();
+  if (w == 0 && m < g.m) {
+    float* C = static_cast<float*>(g.c);
+#pragma unroll
+    for (int j = 0; j < SKINNY_N; ++j) {
+      if (j >= g.n) break;
+      float s = 0.f;
+      for (int q = 0; q < 16; ++q) s += red[q][lane][j];
+      float* cp = C + (long long)m * g.ldc + j;
+      float o = g.alpha * s;
+      if (g.beta != 0.f) o += g.beta * *cp;
+      *cp = o;
+    }
+  }
+}
+}  // namespace
+
+static int gemm_f32_dispatch(const K3mGemm& g, const K3mGemm& gr, int epi_out, bool slabs_only, hipStream_t st) {
+  // g: the problem as launched (epilogue NONE when split); gr: as requested (for the split-K reduction)
+  if (g.n <= SKINNY_N && g.splitk <= 1 && epi_out == K3M_EPI_NONE && g.k >= 256) {
+    hipLaunchKernelGGL(gemm_skinny_kernel, dim3(k3m_cdiv(g.m, 64)), dim3(1024), 0, st, g);
+    K3M_CHECK_LAUNCH();
+    return 0;
   }
   // A: K-contiguous iff a_trans == 0; B: K-contiguous iff b_trans == 1
   const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
@@ -211,6 +300,9 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
     const int vrc = kVariant ? k3m_x6_variant_launch(g, kVariant, st) : -1;
     if (vrc >= 0) {
       rc = vrc;
+    } else if (g.splitk > 1 && g.k <= 256LL * g.splitk && nblocks(g, 256, 128) * g.splitk < 256) {
+      // a small problem split over k (ops.small_splitk): the 64 x 64 tile, one k-slice per grid row
+      rc = launch_x6<64, 64, 2, 2, 16, 2>(g, ak, bk, st);
     } else if (g.splitk > 1 || nblocks(g, 256, 128) >= kPersistMin) {
       if (kPersist) {
         rc = launch_x6_persistent_one(g, (ak || !bk) && prefer_256x256(g), ak, bk, st);
@@ -240,7 +332,8 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
     const long long total = (long long)g.m * g.n;
     const int blocks = (int)std::min<long long>((total + 255) / 256, 2048);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, g.ws, g.splitk, g.m, g.n,
-                       static_cast<float*>(g.c), g.ldc, g.alpha, g.beta);
+                       static_cast<float*>(g.c), g.ldc, g.alpha, g.beta, epi_out, gr.bias, static_cast<float*>(gr.aux),
+                       gr.ldaux);
     K3M_CHECK_LAUNCH();
   }
   return 0;
@@ -361,7 +454,8 @@ extern "C" int k3m_gemm_grouped(const K3mGemm* gs_in, int count, hipStream_t st)
       const long long total = (long long)g.m * g.n;
       const int blocks = (int)std::min<long long>((total + 255) / 256, 2048);
       hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, g.ws, g.splitk, g.m, g.n,
-                         static_cast<float*>(g.c), g.ldc, g.alpha, g.beta);
+                         static_cast<float*>(g.c), g.ldc, g.alpha, g.beta, (int)K3M_EPI_NONE, (const float*)nullptr,
+                         (float*)nullptr, 0LL);
       K3M_CHECK_LAUNCH();
     }
   }

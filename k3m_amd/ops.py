@@ -150,6 +150,12 @@ def gemm(a, a_trans, b, b_trans, c, m, n, k, epi=L.EPI_NONE, bias=None, aux=None
     g.ldaux = _ld(aux) if aux is not None else 0
     g.a, g.b, g.c = ptr(a), ptr(b), ptr(c)
     g.bias, g.aux, g.ws = ptr(bias), ptr(aux), ptr(ws)
+    if (splitk <= 1 and ws is None and _grouper is None and a.dtype == torch.float32 and c.dtype == torch.float32
+            and g.f32_algo == L.F32_SPLIT_BF16X6):
+        s = small_splitk(m, n, k)
+        if s > 1:   # a small fp32 product split over k; the epilogue runs in the split-K reduction
+            splitk, ws = s, torch.empty((s * m * n,), dtype=torch.float32, device=c.device)
+            g.splitk, g.ws = s, ptr(ws)
     g.alpha, g.beta = alpha, beta
     if _grouper is not None:
         _grouper.pending.append((g, (a, b, c, bias, aux, ws)))   # keep the tensors alive until the flush
@@ -274,10 +280,32 @@ def _bf16_fill_split(m, n, k, s0):
     return best if best_t < 0.8 * model(s0) else s0
 
 
+SMALL_SPLITK = os.environ.get("K3M_SMALL_SPLITK", "1") != "0"   # A/B knob
+
+
+def small_splitk(m, n, k):
+    """k-split of a small fp32 product (few 64 x 64 tiles, long k: the m = 64 pooled / gate projections, the
+    389-row region-head GEMMs): one workgroup per (tile, k-slice) instead of one per tile walking all of k, the
+    requested epilogue applied by the split-K reduction.  1 = no split."""
+    if not SMALL_SPLITK or n <= 8 or m <= 8:
+        return 1
+    tiles = ((m + 63) // 64) * ((n + 63) // 64)
+    if tiles >= 128 or k < 512:
+        return 1
+    # few tiles: slices of >= 64 k (4 k-steps of the 64 x 64 tile: a tiny product is a chain of dependent loads, so
+    # fewer steps per workgroup is what makes it faster); more tiles: >= 256 k per slice
+    s = min(k // 256 if tiles >= 64 else k // 64, max(2, 384 // tiles), 32)
+    if ((m + 255) // 256) * ((n + 127) // 128) * s >= 256:
+        return 1
+    return max(1, s)
+
+
 def _splitk(m, n, k, dtype=torch.float32, grouped=False):
     """K-split of a weight-gradient GEMM (C[m,n] summed over k ~ 20k rows): enough blocks to fill
     the 256 CUs in whole waves.  fp32 (bf16x6 kernel) tiles are 256x128 at one block per CU;
     bf16 tiles are 256x256 at one block per CU."""
+    if dtype == torch.float32 and (n <= 8 or m <= 8):
+        return 1   # the skinny kernel (gemm.hip gemm_skinny_kernel) takes n <= 8 whole
     if dtype == torch.float32 and F32_ALGO == L.F32_SPLIT_BF16X6:
         tiles = ((m + 255) // 256) * ((n + 127) // 128)
         if tiles >= 200 or k < 2048:

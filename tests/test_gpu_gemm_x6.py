@@ -127,6 +127,7 @@ def test_grouped_matches_individual(monkeypatch):
     import torch
     from k3m_amd import ops, _lib as L
     monkeypatch.setattr(ops, "SPLITK_FILL", False)
+    monkeypatch.setattr(ops, "SMALL_SPLITK", False)   # grouped problems are never auto-split
     dev = torch.device("cuda")
     torch.manual_seed(0)
     cases = [  # (m, n, k, epi) nt forward problems of the co-attention blocks, ragged edges included
@@ -249,3 +250,80 @@ def test_dgelu_colsum_slabs(dev, dtype, m, n, k):
     # per 32-row group
     grp = torch.nn.functional.pad(c.double(), (0, 0, 0, ns * 32 - m)).view(ns, 32, n).sum(1)
     assert float((slabs.double() - grp).abs().max()) <= 1e-5 * float(grp.abs().max()) + 1e-6
+
+
+@pytest.mark.parametrize("m,n,k", [(64, 768, 768), (64, 1024, 1024), (389, 1024, 1024), (389, 1024, 1601),
+                                   (100, 300, 2048)])
+@pytest.mark.parametrize("epi", ["none", "bias", "gelu", "dgelu", "sigmoid", "beta"])
+def test_small_splitk_epilogues(dev, m, n, k, epi):
+    """Small fp32 products split over k automatically (ops.small_splitk): the epilogue the caller
+    asked for runs in the split-K reduction, with the unsplit kernel's element formulas; compared with the unsplit
+    launch (K3M_SMALL_SPLITK off) and with fp64."""
+    import math
+    from k3m_amd import ops, _lib as L
+    assert ops.small_splitk(m, n, k) > 1
+    g = torch.Generator(device="cpu").manual_seed(m + n + k)
+    A = (torch.rand(m, k, generator=g) * 2 - 1).to(dev)
+    W = ((torch.rand(n, k, generator=g) * 2 - 1) * 0.05).to(dev)
+    bias = (torch.rand(n, generator=g) - 0.5).to(dev)
+    aux0 = torch.randn(m, n, generator=g).to(dev)
+    c0 = torch.randn(m, n, generator=g).to(dev)
+    E = {"none": L.EPI_NONE, "bias": L.EPI_BIAS, "gelu": L.EPI_BIAS_GELU, "dgelu": L.EPI_DGELU,
+         "sigmoid": L.EPI_BIAS_SIGMOID, "beta": L.EPI_BIAS}[epi]
+    alpha, beta = (0.7, 0.5) if epi == "beta" else (1.0, 0.0)
+
+    def run(small):
+        old = ops.SMALL_SPLITK
+        ops.SMALL_SPLITK = small
+        try:
+            c = c0.clone()
+            aux = aux0.clone()
+            ops.gemm(A, 0, W, 1, c, m, n, k, E, bias if E in (L.EPI_BIAS, L.EPI_BIAS_GELU, L.EPI_BIAS_SIGMOID) else None,
+                     aux if E in (L.EPI_BIAS_GELU, L.EPI_DGELU) else None, alpha, beta)
+        finally:
+            ops.SMALL_SPLITK = old
+        torch.cuda.synchronize()
+        return c.double().cpu(), aux.double().cpu()
+    cs, auxs = run(True)
+    cu, auxu = run(False)
+    p = A.double().cpu() @ W.double().cpu().t()
+    b64 = bias.double().cpu()
+    erf = torch.special.erf
+    if E == L.EPI_NONE:
+        ref = p
+    elif E == L.EPI_BIAS:
+        ref = alpha * (p + b64) + beta * c0.double().cpu()
+    elif E == L.EPI_BIAS_GELU:
+        ref = 0.5 * (p + b64) * (1 + erf((p + b64) / math.sqrt(2)))
+        assert float((auxs - (p + b64)).abs().max()) < 1e-5 * float((p + b64).abs().max())
+    elif E == L.EPI_DGELU:
+        x = aux0.double().cpu()
+        ref = p * (0.5 * (1 + erf(x / math.sqrt(2))) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi))
+    else:
+        ref = torch.sigmoid(p + b64)
+    scale = float(ref.abs().max())
+    assert float((cs - ref).abs().max()) < 1e-5 * scale, epi
+    assert float((cs - cu).abs().max()) < 1e-5 * scale, epi   # the split and the unsplit launch agree
+
+
+@pytest.mark.parametrize("at,bt", [(1, 0), (0, 0), (0, 1), (1, 1)])
+@pytest.mark.parametrize("m,n,k", [(1024, 5, 2368), (300, 8, 700), (77, 1, 256)])
+def test_skinny_gemm(dev, m, n, k, at, bt):
+    """n <= 8 fp32 products (the image-location weight gradient, tn 1024 x 5 x 2,368) on the skinny kernel: exact
+    fp32 FMAs against fp64, alpha / beta, run-to-run bit-identical."""
+    from k3m_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(m * 7 + n)
+    A = torch.rand(m, k, generator=g) * 2 - 1
+    Bm = torch.rand(k, n, generator=g) * 2 - 1
+    c0 = torch.randn(m, n, generator=g)
+    a = (A.t().contiguous() if at else A).to(dev)
+    b = (Bm.t().contiguous() if bt else Bm).to(dev)
+    outs = []
+    for _ in range(2):
+        c = c0.clone().to(dev)
+        ops.gemm(a, at, b, bt, c, m, n, k, alpha=0.5, beta=1.0)
+        torch.cuda.synchronize()
+        outs.append(c.cpu())
+    ref = 0.5 * (A.double() @ Bm.double()) + c0.double()
+    assert torch.equal(outs[0], outs[1])
+    assert float((outs[0].double() - ref).abs().max()) < 1e-5 * float(ref.abs().max())
