@@ -142,11 +142,31 @@ __device__ __forceinline__ float block_max(float v, float* red) {
   return s;
 }
 
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// fp32 erf-GELU (the reference's gelu, x * 0.5 * (1 + erf(x / sqrt 2)), vilbert_k3m.py) and its derivative in a
+// branch-free form: Phi(x) from erfc(z) = t exp(-z^2 + P(t)), z = |x| / sqrt 2, t = 1 / (1 + z / 2) (the
+// Chebyshev fit of Numerical Recipes' erfcc, fractional error < 1.2e-7 for every z).  In fp32 (numpy sweep of
+// x in [-12, 12] against scipy, float64 reference): GELU max absolute error 1.6e-7 and max relative error 3.9e-6
+// for |x| < 5, where the erff form's 1 + erf cancels (6.8e-7 absolute, 4.8 % relative in the left tail).  ocml's
+// erff takes a divergent two-branch path (~35 VALU per element in the GEMM epilogues); this is ~18, no branch.
+__device__ __forceinline__ float phi_cdf(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
+  float p = fmaf(0.17087277f, t, -0.82215223f);
+  p = fmaf(p, t, 1.48851587f);
+  p = fmaf(p, t, -1.13520398f);
+  p = fmaf(p, t, 0.27886807f);
+  p = fmaf(p, t, -0.18628806f);
+  p = fmaf(p, t, 0.09678418f);
+  p = fmaf(p, t, 0.37409196f);
+  p = fmaf(p, t, 1.00002368f);
+  const float arg = fmaf(-z, z, fmaf(p, t, -1.26551223f));
+  const float q = 0.5f * t * __builtin_amdgcn_exp2f(arg * 1.4426950408889634f);   // Phi(-|x|)
+  return x >= 0.f ? 1.0f - q : q;
+}
+__device__ __forceinline__ float gelu_f(float x) { return x * phi_cdf(x); }
 __device__ __forceinline__ float dgelu_f(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.3989422804014327f * expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  const float pdf = 0.3989422804014327f * __builtin_amdgcn_exp2f(-0.72134752044448170f * x * x);   // exp(-x^2/2)
+  return fmaf(x, pdf, phi_cdf(x));
 }
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 

@@ -228,24 +228,30 @@ extern "C" int k3m_gemm(const K3mGemm* gp, hipStream_t st) {
 
 namespace {
 // fp32 C[m, n] (n <= 8) = alpha A B + beta C for the skinny products of the step (the 5-column image-location
-// weight gradient, tn 1024 x 5 x 2,368): exact fp32 FMAs, 64 rows per workgroup, the k range dealt to the 16
-// waves in fixed interleaved order and reduced through LDS in wave order (deterministic).  The tile kernels
-// gave such a product 1-2 % of one CU's MFMA rate (64 us).
+// weight gradient, tn 1024 x 5 x 2,368): exact fp32 FMAs, 64 rows per workgroup.  Split over k (ops.small_splitk)
+// each grid row y computes the k-slice y into its fp32 slab (ws + y m n, reduced in slab order with the epilogue by
+// splitk_reduce_kernel), so the 16 row blocks of that product fill 256 workgroups; inside a workgroup the slice is
+// dealt to the 4 waves in contiguous ranges and reduced through LDS in wave order (deterministic).  The 64 x 64
+// tile kernels gave such a product 1-2 % of one CU's MFMA rate (64 us); unsplit, 16 workgroups were latency-bound.
 constexpr int SKINNY_N = 8;
 constexpr int SKINNY_U = 8;   // k values per thread in flight
-__global__ __launch_bounds__(1024) void gemm_skinny_kernel(K3mGemm g) {
-  __shared__ float red[16][64][SKINNY_N + 1];
+constexpr int SKINNY_W = 4;   // waves per workgroup
+__global__ __launch_bounds__(64 * SKINNY_W) void gemm_skinny_kernel(K3mGemm g) {
+  __shared__ float red[SKINNY_W][64][SKINNY_N + 1];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int m = blockIdx.x * 64 + lane;
   const int mc = min(m, g.m - 1);   // clamped row: every lane loads, the store is masked
   const float* A = static_cast<const float*>(g.a);
   const float* B = static_cast<const float*>(g.b);
+  const int splits = max(g.splitk, 1);
+  const int kslice = (g.k + splits - 1) / splits;
+  const int ks0 = blockIdx.y * kslice, ks1 = min(g.k, ks0 + kslice);
   float acc[SKINNY_N];
 #pragma unroll
   for (int j = 0; j < SKINNY_N; ++j) acc[j] = 0.f;
-  // wave w owns the contiguous k range [k0, k1); SKINNY_U loads of A issued before their FMAs
-  const int per = (g.k + 15) / 16, k0 = w * per, k1 = min(g.k, k0 + per);
+  // wave w owns the contiguous k range [k0, k1) of the slice; SKINNY_U loads of A issued before their FMAs
+  const int per = (ks1 - ks0 + SKINNY_W - 1) / SKINNY_W, k0 = ks0 + w * per, k1 = min(ks1, k0 + per);
   for (int kb = k0; kb < k1; kb += SKINNY_U) {
     float av[SKINNY_U];
 #pragma unroll
@@ -266,36 +272,38 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(K3mGemm g) {
   for (int j = 0; j < SKINNY_N; ++j) red[w][lane][j] = acc[j];
   __syncthreads();
   if (w == 0 && m < g.m) {
-    float* C = static_cast<float*>(g.c);
+    const bool slab = splits > 1;
+    float* C = slab ? static_cast<float*>(g.ws) + (long long)blockIdx.y * g.m * g.n : static_cast<float*>(g.c);
+    const long long ldc = slab ? g.n : g.ldc;
 #pragma unroll
     for (int j = 0; j < SKINNY_N; ++j) {
       if (j >= g.n) break;
       float s = 0.f;
-      for (int q = 0; q < 16; ++q) s += red[q][lane][j];
-      float* cp = C + (long long)m * g.ldc + j;
-      float o = g.alpha * s;
-      if (g.beta != 0.f) o += g.beta * *cp;
-      *cp = o;
+#pragma unroll
+      for (int q = 0; q < SKINNY_W; ++q) s += red[q][lane][j];
+      float* cp = C + (long long)m * ldc + j;
+      if (slab) {
+        *cp = s;
+      } else {
+        float o = g.alpha * s;
+        if (g.beta != 0.f) o += g.beta * *cp;
+        *cp = o;
+      }
     }
   }
 }
 }  // namespace
 
-static int gemm_f32_dispatch(const K3mGemm& g, const K3mGemm& gr, int epi_out, bool slabs_only, hipStream_t st) {
-  // g: the problem as launched (epilogue NONE when split); gr: as requested (for the split-K reduction)
-  if (g.n <= SKINNY_N && g.splitk <= 1 && epi_out == K3M_EPI_NONE && g.k >= 256) {
-    hipLaunchKernelGGL(gemm_skinny_kernel, dim3(k3m_cdiv(g.m, 64)), dim3(1024), 0, st, g);
-    K3M_CHECK_LAUNCH();
-    return 0;
-  }
+// the tile kernel for one fp32 problem (launch only; the split-K reduction is the caller's)
+static int gemm_f32_tiles(const K3mGemm& g, hipStream_t st) {
   // A: K-contiguous iff a_trans == 0; B: K-contiguous iff b_trans == 1
+  int rc;
   const bool ak = g.a_trans == 0, bk = g.b_trans == 1;
   const bool av = aligned16(g.a) && (g.lda % 4 == 0) && ((ak ? g.k : g.m) % 4 == 0);
   const bool bv = aligned16(g.b) && (g.ldb % 4 == 0) && ((bk ? g.k : g.n) % 4 == 0);
   const bool vec = av && bv;
   // tile choice: the largest tile that still fills the 256 CUs; small co-attention GEMMs
   // (2,304-8,192 rows) otherwise leave CUs idle
-  int rc;
   if (vec && g.f32_algo == K3M_F32_SPLIT_BF16X6) {
     const int vrc = kVariant ? k3m_x6_variant_launch(g, kVariant, st) : -1;
     if (vrc >= 0) {
@@ -326,6 +334,19 @@ static int gemm_f32_dispatch(const K3mGemm& g, const K3mGemm& gr, int epi_out, b
   else if (g.splitk > 1 || nblocks(g, 128, 128) >= 384) rc = launch_tile<128, 128, 2, 2, 2>(g, ak, bk, vec, st);
   else if (nblocks(g, 64, 128) >= 384) rc = launch_tile<64, 128, 2, 2, 2>(g, ak, bk, vec, st);
   else rc = launch_tile<64, 64, 2, 2, 2>(g, ak, bk, vec, st);
+  return rc;
+}
+
+static int gemm_f32_dispatch(const K3mGemm& g, const K3mGemm& gr, int epi_out, bool slabs_only, hipStream_t st) {
+  // g: the problem as launched (epilogue NONE when split); gr: as requested (for the split-K reduction)
+  int rc;
+  if (g.n <= SKINNY_N && (g.splitk > 1 || epi_out == K3M_EPI_NONE) && g.k >= 256) {
+    hipLaunchKernelGGL(gemm_skinny_kernel, dim3(k3m_cdiv(g.m, 64), std::max(g.splitk, 1)), dim3(64 * SKINNY_W), 0,
+                       st, g);
+    rc = 0;
+  } else {
+    rc = gemm_f32_tiles(g, st);
+  }
   if (rc) return rc;
   K3M_CHECK_LAUNCH();
   if (g.splitk > 1 && !slabs_only) {

@@ -287,10 +287,17 @@ def small_splitk(m, n, k):
     """k-split of a small fp32 product (few 64 x 64 tiles, long k: the m = 64 pooled / gate projections, the
     389-row region-head GEMMs): one workgroup per (tile, k-slice) instead of one per tile walking all of k, the
     requested epilogue applied by the split-K reduction.  1 = no split."""
-    if not SMALL_SPLITK or n <= 8 or m <= 8:
+    if not SMALL_SPLITK or m <= 8:
         return 1
+    if n <= 8:
+        # the skinny kernel (gemm.hip gemm_skinny_kernel, 64 rows per workgroup): k-slices of >= 128 until the
+        # row blocks x slices fill 256 workgroups (loc wgrad 1,024 x 5 x 2,368: 16 x 16)
+        if k < 256:
+            return 1
+        return max(1, min(k // 128, max(1, 256 // ((m + 63) // 64)), 64))
     tiles = ((m + 63) // 64) * ((n + 63) // 64)
-    if tiles >= 128 or k < 512:
+    # >= 64 tiles at k = 1,024 (the 389-row region heads) measured slower split (0.030 -> 0.040 ms)
+    if tiles >= 128 or k < 512 or (tiles >= 64 and k < 1536):
         return 1
     # few tiles: slices of >= 64 k (4 k-steps of the 64 x 64 tile: a tiny product is a chain of dependent loads, so
     # fewer steps per workgroup is what makes it faster); more tiles: >= 256 k per slice
@@ -305,7 +312,7 @@ def _splitk(m, n, k, dtype=torch.float32, grouped=False):
     the 256 CUs in whole waves.  fp32 (bf16x6 kernel) tiles are 256x128 at one block per CU;
     bf16 tiles are 256x256 at one block per CU."""
     if dtype == torch.float32 and (n <= 8 or m <= 8):
-        return 1   # the skinny kernel (gemm.hip gemm_skinny_kernel) takes n <= 8 whole
+        return 1   # n <= 8: the skinny kernel, split by small_splitk inside gemm()
     if dtype == torch.float32 and F32_ALGO == L.F32_SPLIT_BF16X6:
         tiles = ((m + 255) // 256) * ((n + 127) // 128)
         if tiles >= 200 or k < 2048:

@@ -252,7 +252,7 @@ def test_dgelu_colsum_slabs(dev, dtype, m, n, k):
     assert float((slabs.double() - grp).abs().max()) <= 1e-5 * float(grp.abs().max()) + 1e-6
 
 
-@pytest.mark.parametrize("m,n,k", [(64, 768, 768), (64, 1024, 1024), (389, 1024, 1024), (389, 1024, 1601),
+@pytest.mark.parametrize("m,n,k", [(64, 768, 768), (64, 1024, 1024), (389, 1024, 2048), (389, 1024, 1601),
                                    (100, 300, 2048)])
 @pytest.mark.parametrize("epi", ["none", "bias", "gelu", "dgelu", "sigmoid", "beta"])
 def test_small_splitk_epilogues(dev, m, n, k, epi):
@@ -306,12 +306,15 @@ def test_small_splitk_epilogues(dev, m, n, k, epi):
     assert float((cs - cu).abs().max()) < 1e-5 * scale, epi   # the split and the unsplit launch agree
 
 
+@pytest.mark.parametrize("small", [True, False])
 @pytest.mark.parametrize("at,bt", [(1, 0), (0, 0), (0, 1), (1, 1)])
-@pytest.mark.parametrize("m,n,k", [(1024, 5, 2368), (300, 8, 700), (77, 1, 256)])
-def test_skinny_gemm(dev, m, n, k, at, bt):
-    """n <= 8 fp32 products (the image-location weight gradient, tn 1024 x 5 x 2,368) on the skinny kernel: exact
-    fp32 FMAs against fp64, alpha / beta, run-to-run bit-identical."""
+@pytest.mark.parametrize("m,n,k", [(1024, 5, 2368), (300, 8, 700), (77, 1, 256), (64, 3, 9000)])
+def test_skinny_gemm(dev, m, n, k, at, bt, small, monkeypatch):
+    """n <= 8 fp32 products (the image-location weight gradient, tn 1024 x 5 x 2,368) on the skinny kernel, whole
+    and split over k into slabs (ops.small_splitk): exact fp32 FMAs against fp64, alpha / beta, run-to-run
+    bit-identical."""
     from k3m_amd import ops
+    monkeypatch.setattr(ops, "SMALL_SPLITK", small)
     g = torch.Generator(device="cpu").manual_seed(m * 7 + n)
     A = torch.rand(m, k, generator=g) * 2 - 1
     Bm = torch.rand(k, n, generator=g) * 2 - 1
@@ -327,3 +330,19 @@ def test_skinny_gemm(dev, m, n, k, at, bt):
     ref = 0.5 * (A.double() @ Bm.double()) + c0.double()
     assert torch.equal(outs[0], outs[1])
     assert float((outs[0].double() - ref).abs().max()) < 1e-5 * float(ref.abs().max())
+
+
+def test_skinny_split_epilogue(dev):
+    """A split skinny product with the bias + GELU epilogue applied in the split-K reduction."""
+    from k3m_amd import ops, _lib as L
+    assert ops.small_splitk(1024, 5, 2368) > 1
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = (torch.rand(1024, 2368, generator=g) * 2 - 1).to(dev)
+    W = (torch.rand(5, 2368, generator=g) * 0.1 - 0.05).to(dev)
+    b = torch.randn(5, generator=g).to(dev)
+    pre = torch.empty(1024, 5, device=dev)
+    y = ops.linear(x, W, b, epi=L.EPI_BIAS_GELU, aux=pre)
+    r = x.double() @ W.double().t() + b.double()
+    assert float((pre.double() - r).abs().max()) < 1e-5 * float(r.abs().max())
+    ref = torch.nn.functional.gelu(r)
+    assert float((y.double() - ref).abs().max()) < 1e-5 * float(ref.abs().max())

@@ -72,6 +72,32 @@ def test_gemm_epilogues(dev):
     assert _rel(dx, xr.grad) < 1e-5
 
 
+def test_gelu_accuracy_fp64(dev):
+    """The branch-free erfc-form GELU / dGELU (common.h phi_cdf) against float64 erf over [-12, 12]: the
+    epilogue GELU (a GEMM with an identity weight) and the elementwise dGELU kernel.  Bounds: absolute 5e-7
+    everywhere, relative 2e-5 for |x| < 5 (the erff form's 1 + erf cancels to ~5 % relative in the left tail)."""
+    from k3m_amd import ops, _lib as L
+    x = torch.linspace(-12, 12, 64 * 1024, device=dev, dtype=torch.float64)
+    xf = x.float().reshape(-1, 64).contiguous()
+    eye = torch.eye(64, device=dev)
+    pre = torch.empty_like(xf)
+    y = ops.linear(xf, eye, torch.zeros(64, device=dev), epi=L.EPI_BIAS_GELU, aux=pre)
+    assert _rel(pre, xf) < 1e-7
+    x64 = pre.double()           # the epilogue's input, whatever the GEMM rounded
+    cdf = 0.5 * (1 + torch.erf(x64 / math.sqrt(2)))
+    ref_g = x64 * cdf
+    ref_d = cdf + x64 * torch.exp(-0.5 * x64 * x64) / math.sqrt(2 * math.pi)
+    xf = pre
+    err = (y.double() - ref_g).abs()
+    assert float(err.max()) < 5e-7
+    mid = x64.abs() < 5
+    assert float((err[mid] / ref_g[mid].abs().clamp_min(1e-30)).max()) < 2e-5
+    d = torch.empty_like(xf)
+    ops.dgelu(torch.ones_like(xf), xf, d)
+    derr = (d.double() - ref_d).abs()
+    assert float(derr.max()) < 5e-7
+
+
 def test_wgrad_colsum(dev):
     from k3m_amd import ops
     dy = torch.randn(20992, 768, device=dev)
