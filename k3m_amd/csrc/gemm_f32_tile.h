@@ -240,6 +240,11 @@ __device__ __forceinline__ void ld8(const float* p, float (&v)[8]) {
   v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
 }
 __device__ __forceinline__ void st8(float* p, const float (&v)[8]) {
+#ifdef K3M_LAB_NO_STORE   // lab only (scripts/lab/lab_build.sh): timing without the epilogue's stores, math kept
+#pragma unroll
+  for (int e = 0; e < 8; ++e) asm volatile("" ::"v"(v[e]));
+  return;
+#endif
   *reinterpret_cast<floatx4*>(p) = floatx4{v[0], v[1], v[2], v[3]};
   *reinterpret_cast<floatx4*>(p + 4) = floatx4{v[4], v[5], v[6], v[7]};
 }
