@@ -245,7 +245,9 @@ def _attn_ref(q, k, v, mask, nh):
 @pytest.mark.parametrize("lq,lk,nh,hd", [(36, 36, 12, 64), (128, 128, 12, 64), (37, 37, 8, 128), (36, 37, 8, 128),
                                          (37, 128, 8, 128), (128, 36, 8, 96), (36, 128, 8, 96),
                                          # ragged d = 64 shapes of the bf16x6 key-major backward (attn_bwd_x6km_kernel)
-                                         (65, 65, 4, 64), (100, 128, 3, 64), (33, 50, 2, 64), (128, 40, 2, 64)])
+                                         (65, 65, 4, 64), (100, 128, 3, 64), (33, 50, 2, 64), (128, 40, 2, 64),
+                                         # d = 128 with up to 128 keys on the two-pass x6 forward staging
+                                         (64, 128, 2, 128), (60, 97, 3, 128), (96, 65, 2, 128)])
 def test_attention(dev, lq, lk, nh, hd):
     from k3m_amd import ops
     B = 5
