@@ -10,6 +10,8 @@ import os
 
 import torch  # noqa: F401  (loads the HIP runtime first)
 
+from . import debug as _debug
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # K3M_LIB: another build of the same library (same-box A/B of two builds, scripts/ab_lib.sh)
 LIB_PATH = os.environ.get("K3M_LIB") or os.path.join(_HERE, "libk3m_hip.so")
@@ -161,3 +163,5 @@ def call(name, *args):
     rc = fn(*args)
     if rc != 0:
         raise RuntimeError("%s failed with status %d (%s)" % (name, rc, "bad argument" if rc == 1 else "hip error %d" % -rc))
+    if _debug.ON:
+        _debug.sync(name)

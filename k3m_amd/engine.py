@@ -29,6 +29,7 @@ import os
 
 import torch
 
+from . import debug
 from . import _lib as L
 from . import ops
 from .params import flat_layout
@@ -607,6 +608,8 @@ class K3MEngine(object):
         zero-triple fallback crosses items, and it is kept inside each group."""
         c = self.cfg
         fp = self.fp
+        if debug.ON:
+            debug.check_batch(batch, c, ent_neg, val_neg)
         fp.refresh_shadow()
         dev = self.device
         H, Hv = self.H, self.Hv

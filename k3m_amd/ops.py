@@ -6,6 +6,7 @@ import os
 import torch
 
 from . import _lib as L
+from . import debug as _debug
 from ._lib import call, ptr, stream
 
 _DT = {torch.float32: L.F32, torch.bfloat16: L.BF16}
@@ -485,6 +486,10 @@ def ln_bwd(dy, xhat, rstd, gamma, dres, dx, dgamma, dbeta, p_in=0.0, p_out=0.0, 
 
 def embed_fwd(ids, tt, word, pos, typ, gamma, beta, y0, y1, y2, xhat, rstd, p_out, seed, off, eps=1e-12):
     nseq, ln = ids.shape
+    if _debug.ON:
+        _debug.check_range(ids, 0, word.shape[0], "embedding ids")
+        _debug.check_range(tt, 0, typ.shape[0], "token type ids")
+        _debug.check_len(ln, pos.shape[0], "sequence length")
     call("k3m_embed_fwd", ptr(ids), ptr(tt), ptr(word), ptr(pos), ptr(typ), ptr(gamma), ptr(beta), ptr(y0), ptr(y1),
          ptr(y2), ptr(xhat), ptr(rstd), nseq, ln, word.shape[1], eps, p_out, seed, off, dt(y0), stream())
 
@@ -632,9 +637,13 @@ def convert(x, y, accumulate=False, alpha=1.0):
 
 
 def gather_rows(src, idx, n, out):
+    if _debug.ON:
+        _debug.check_range(idx[:n], 0, src.shape[0], "gather_rows index")
     call("k3m_gather_rows", ptr(src), _ld(src), ptr(idx), n, src.shape[1], ptr(out), _ld(out), dt(src), stream())
 
 
 def scatter_add_rows(src, idx, n, dst):
+    if _debug.ON:
+        _debug.check_range(idx[:n], 0, dst.shape[0], "scatter_add_rows index")
     call("k3m_scatter_add_rows", ptr(src), _ld(src), ptr(idx), n, src.shape[1], ptr(dst), _ld(dst), dt(src),
          stream())
