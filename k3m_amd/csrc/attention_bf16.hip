@@ -54,7 +54,11 @@ __device__ __forceinline__ void stage(uint16_t* img, const uint16_t* __restrict_
 }
 
 // ------------------------------------------------------------------ forward
-template <int HD>
+// PAIR (lq, lk <= 64: the 36-token text, 37-region image and text<->image heads): two heads per workgroup,
+// waves 0-1 on head 2p, waves 2-3 on head 2p + 1, so every wave has queries and a workgroup's one memory round
+// trip stages two heads (one head per workgroup left two of its four waves idle and doubled the number of
+// latency-bound workgroups).  Image row 64 hh + r holds row r of head hh; the key mask is the sequence's, shared.
+template <int HD, bool PAIR = false>
 __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __restrict__ q, long long ldq,
                                                           const uint16_t* __restrict__ k, long long ldk,
                                                           const uint16_t* __restrict__ v, long long ldv,
@@ -65,8 +69,10 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __rest
   // head dim 96 rows are stored 128 wide (the 16-chunk swizzle) and only 12 chunks are used
   constexpr int NCL = HD / 8, NC = HD == 96 ? 16 : HD / 8, DT = HD / 32, KS = HD / 16;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  const int s = blockIdx.x / nh, h = blockIdx.x % nh;
-  const int LQ = (lq + 31) & ~31, LK = (lk + 31) & ~31;
+  const int nhw = PAIR ? (nh + 1) >> 1 : nh;
+  const int s = blockIdx.x / nhw, h0 = PAIR ? 2 * (blockIdx.x % nhw) : blockIdx.x % nhw;
+  const int LQh = (lq + 31) & ~31, LKh = (lk + 31) & ~31;     // one head's padded rows
+  const int LQ = PAIR ? MAXL : LQh, LK = PAIR ? MAXL : LKh;   // image rows
   uint16_t* Qs = smem;
   constexpr int HW = NC * 8;   // image row width
   uint16_t* Ks = Qs + LQ * HW;
@@ -74,7 +80,6 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __rest
   float* msk = reinterpret_cast<float*>(Vs + LK * HW);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
   const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
-  const int hoff = h * HD;
 
   {
     // every global load (Q, K, V chunks, mask) issued before the first LDS write: one memory round trip
@@ -83,20 +88,23 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __rest
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int e = threadIdx.x + u * NT, i = e / NCL, c = e % NCL;
+      const int hh = PAIR ? i >> 6 : 0, li = PAIR ? i & 63 : i;
+      const bool hok = !PAIR || h0 + hh < nh;
+      const int ho = min(h0 + hh, nh - 1) * HD;
       // unconditional loads from clamped rows, zeroed after the load: a load under a per-element runtime
       // condition makes hipcc branch around it with a vmcnt(0) inside (every load one round trip)
-      const bool qv = i < lq, kv = i < lk;
-      const long long qo = qrow0 + min(i, lq - 1), ko = krow0 + min(i, lk - 1);
-      const uint4 a = *reinterpret_cast<const uint4*>(q + qo * ldq + hoff + 8 * c);
-      const uint4 b = *reinterpret_cast<const uint4*>(k + ko * ldk + hoff + 8 * c);
-      const uint4 d = *reinterpret_cast<const uint4*>(v + ko * ldv + hoff + 8 * c);
+      const bool qv = hok && li < lq, kv = hok && li < lk;
+      const long long qo = qrow0 + min(li, lq - 1), ko = krow0 + min(li, lk - 1);
+      const uint4 a = *reinterpret_cast<const uint4*>(q + qo * ldq + ho + 8 * c);
+      const uint4 b = *reinterpret_cast<const uint4*>(k + ko * ldk + ho + 8 * c);
+      const uint4 d = *reinterpret_cast<const uint4*>(v + ko * ldv + ho + 8 * c);
       rq[u] = keep_if(qv, a);
       rk[u] = keep_if(kv, b);
       rv[u] = keep_if(kv, d);
     }
     const int t = threadIdx.x;
     float mv = 0.f;
-    if (t < LK) mv = t < lk ? (kmask ? kmask[krow0 + t] : 0.f) : -INFINITY;
+    if (t < LKh) mv = t < lk ? (kmask ? kmask[krow0 + t] : 0.f) : -INFINITY;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int e = threadIdx.x + u * NT, i = e / NCL, c = e % NCL;
@@ -106,12 +114,15 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __rest
         *reinterpret_cast<uint4*>(Vs + ioff<NC>(i, c)) = rv[u];
       }
     }
-    if (t < LK) msk[t] = mv;
+    if (t < LKh) msk[t] = mv;
   }
   __syncthreads();
-  const int i0 = 32 * w;
-  if (i0 >= LQ) return;
-  const int NJT = LK / 32;
+  const int hh = PAIR ? w >> 1 : 0, h = h0 + hh;
+  const int rb = 64 * hh;                       // image row of this wave's head's row 0
+  const int i0 = 32 * (PAIR ? (w & 1) : w);     // the wave's query tile (head-local)
+  if (h >= nh || i0 >= LQh) return;
+  const int hoff = h * HD;
+  const int NJT = LKh / 32;
   floatx16 S[MAXL / 32];
 #pragma unroll
   for (int jt = 0; jt < MAXL / 32; ++jt) {
@@ -119,8 +130,8 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __rest
       floatx16 a = zero16();
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
-        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag<NC>(Ks, 32 * jt, ks, lane), rowfrag<NC>(Qs, i0, ks, lane),
-                                                     a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag<NC>(Ks, rb + 32 * jt, ks, lane),
+                                                     rowfrag<NC>(Qs, rb + i0, ks, lane), a, 0, 0, 0);
       S[jt] = a;
     }
   }
@@ -175,7 +186,8 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __rest
       if (jt < NJT) {
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2)
-          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(accfrag(S[jt], s2), trfrag<NC, true>(Vs, 32 * jt + 16 * s2, 32 * dt, lane),
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(accfrag(S[jt], s2),
+                                                       trfrag<NC, true>(Vs, rb + 32 * jt + 16 * s2, 32 * dt, lane),
                                                        o, 0, 0, 0);
       }
     // o[r] = O[i0 + (r&3) + 8(r>>2) + 4kl][32 dt + cl]
@@ -613,6 +625,7 @@ void set_attrs() {
     (void)hipFuncSetAttribute((const void*)flash_fwd_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_fwd_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_fwd_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_fwd_kernel<64, true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_bwd_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_bwd_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_bwd_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
@@ -630,6 +643,9 @@ bool vec_ok(const void* p, long long ld) { return (reinterpret_cast<uintptr_t>(p
 
 }  // namespace
 
+// two heads per forward workgroup for lq, lk <= 64 (flash_fwd_kernel PAIR); K3M_FLASH_PAIR=0 keeps one (A/B knob)
+static const bool kFlashPair = k3m_env_flag("K3M_FLASH_PAIR", true);
+
 // the key-major backward (flash_bwd_km_kernel); K3M_FLASH_BWD_KM=0 keeps the P / dS image kernel
 static const bool kFlashBwdKM = k3m_env_flag("K3M_FLASH_BWD_KM", true);
 
@@ -641,22 +657,22 @@ extern "C" int k3m_flash_attn_fwd(const void* q, long long ldq, const void* k, l
   K3M_ARG(lq > 0 && lq <= MAXL && lk > 0 && lk <= MAXL && (hd == 64 || hd == 96 || hd == 128) && nh > 0 && nseq >= 0);
   K3M_ARG(vec_ok(q, ldq) && vec_ok(k, ldk) && vec_ok(v, ldv));
   if (nseq == 0) return 0;
-  const size_t lds = fwd_lds(lq, lk, hd);
+  // (d = 64 only: a d = 128 pair needs 98 KB of LDS, one workgroup per CU = 2 heads, against 3 single-head
+  // workgroups of 49 KB)
+  const bool pair = kFlashPair && hd == 64 && lq <= 64 && lk <= 64 && nh > 1;
+  const size_t lds = pair ? fwd_lds(MAXL, MAXL, hd) : fwd_lds(lq, lk, hd);
   K3M_ARG(lds <= (size_t)LDS_MAX);
   set_attrs();
-#define K3M_FLASH_FWD(HD_)                                                                                       \
-  hipLaunchKernelGGL(flash_fwd_kernel<HD_>, dim3(nseq * nh), dim3(NT), lds, st, (const uint16_t*)q, ldq,            \
+  const int nblk = nseq * (pair ? (nh + 1) / 2 : nh);
+#define K3M_FLASH_FWD(HD_, P_)                                                                                   \
+  hipLaunchKernelGGL((flash_fwd_kernel<HD_, P_>), dim3(nblk), dim3(NT), lds, st, (const uint16_t*)q, ldq,           \
                      (const uint16_t*)k, ldk, (const uint16_t*)v, ldv, kmask, (uint16_t*)ctx, ldc, lse, lq, lk, nh, \
                      scale, p_drop, seed, off)
-  if (hd == 96) K3M_FLASH_FWD(96);
-  else if (hd == 64)
-    hipLaunchKernelGGL(flash_fwd_kernel<64>, dim3(nseq * nh), dim3(NT), lds, st, (const uint16_t*)q, ldq,
-                       (const uint16_t*)k, ldk, (const uint16_t*)v, ldv, kmask, (uint16_t*)ctx, ldc, lse, lq, lk, nh,
-                       scale, p_drop, seed, off);
-  else
-    hipLaunchKernelGGL(flash_fwd_kernel<128>, dim3(nseq * nh), dim3(NT), lds, st, (const uint16_t*)q, ldq,
-                       (const uint16_t*)k, ldk, (const uint16_t*)v, ldv, kmask, (uint16_t*)ctx, ldc, lse, lq, lk, nh,
-                       scale, p_drop, seed, off);
+  if (hd == 96) K3M_FLASH_FWD(96, false);
+  else if (hd == 64) {
+    if (pair) K3M_FLASH_FWD(64, true); else K3M_FLASH_FWD(64, false);
+  } else K3M_FLASH_FWD(128, false);
+#undef K3M_FLASH_FWD
   K3M_CHECK_LAUNCH();
   return 0;
 }

@@ -206,7 +206,7 @@ def test_attention_bf16(dev, lq, lk, nh, hd):
                                          (128, 37, 8, 128), (37, 128, 8, 128), (128, 36, 8, 128), (20, 90, 4, 64),
                                          (128, 36, 8, 96), (36, 128, 8, 96),
                                          (1, 5, 2, 64), (128, 101, 8, 128), (128, 128, 8, 128), (96, 128, 12, 64),
-                                         (65, 128, 4, 64), (128, 128, 8, 96), (33, 64, 3, 64),
+                                         (65, 128, 4, 64), (128, 128, 8, 96), (33, 64, 3, 64), (64, 64, 5, 64), (40, 17, 7, 64),
                                          # L > 128: attention_flash_long.hip (the config-5 shapes
                                          # PV 320 self-attention, PV <-> title d = 96, PV <-> image d = 128), ragged
                                          # and multi-key-group heads, the 512 maximum, a single query
