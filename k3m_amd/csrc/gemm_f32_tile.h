@@ -245,8 +245,13 @@ __device__ __forceinline__ void st8(float* p, const float (&v)[8]) {
   for (int e = 0; e < 8; ++e) asm volatile("" ::"v"(v[e]));
   return;
 #endif
+#ifdef K3M_LAB_NT_STORE   // lab (scripts/lab/lab_build.sh): streaming stores, no dirty L2 lines left at the kernel's end
+  __builtin_nontemporal_store(floatx4{v[0], v[1], v[2], v[3]}, reinterpret_cast<floatx4*>(p));
+  __builtin_nontemporal_store(floatx4{v[4], v[5], v[6], v[7]}, reinterpret_cast<floatx4*>(p + 4));
+#else
   *reinterpret_cast<floatx4*>(p) = floatx4{v[0], v[1], v[2], v[3]};
   *reinterpret_cast<floatx4*>(p + 4) = floatx4{v[4], v[5], v[6], v[7]};
+#endif
 }
 
 template <int EPI>

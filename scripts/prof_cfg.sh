@@ -11,6 +11,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out"
 tr=$(find "$out" -name "run_kernel_trace.csv" | head -1)
 st=$(find "$out" -name "run_kernel_stats.csv" | head -1)
 python scripts/step_time_split.py "$tr" "$steps" 40 30 > "$out/step_split.txt" 2>&1
+python scripts/step_gaps.py "$tr" "$steps" 5 30 > "$out/step_gaps.txt" 2>&1
 cp "$st" "$out/kernel_stats.csv"
 rm -f "$tr"
 timeout -k 10 400 python scripts/gemm_calls.py --config "$cfg" --top 60 > "$out/gemm_calls.txt" 2>&1
