@@ -3,8 +3,8 @@ reasonable time; bs=2 slices of configs[3]/[4] are pinned against reference gold
 test_gpu_parity.py: cfg4_bs2, cfg5_bs2).  Size-independent properties:
 
 * configs[2] (bf16, bs=64): the bf16 step computes the same step as the fp32 step on the same
-  inputs and weights: losses within BF16_LOSS_RTOL, total gradient cosine >= 0.99 and norm within
-  5e-2 (mixed precision, tolerances as in test_gpu_parity's bf16 bar);
+  inputs and weights: losses within 2e-3, total gradient cosine >= 0.995 and norm within 1e-2
+  (bars about 10x / 2x / 4x above the measured values; test_bf16_matches_fp32_step, also for configs 4 and 5);
 * configs[3] (12/6/6 layers, seq_len 128, 100 boxes, bf16, bs=256) and configs[4] (50 PV triples in
   a 320-token PV sequence, bf16, bs=128): two train-mode Trainer steps (dropout, device gumbel noise
   and LPM negatives, AdamW) are finite and the peak device memory of the step is reported and fits
@@ -49,9 +49,11 @@ CMP = {
 @pytest.mark.parametrize("name", sorted(CMP))
 def test_bf16_matches_fp32_step(dev, name):
     """The bf16 step against the fp32 step on the same inputs and weights at each bf16 config's full size (VERDICT r4
-    item 5b: configs 4 and 5 were only checked for finiteness): losses within 1e-2 relative, total gradient cosine
-    >= 0.99, norm within 5e-2.  Config 5's PV attention runs attention_flash_long.hip in bf16 and the exact-fp32
-    attention_long.hip in fp32."""
+    item 5b: configs 4 and 5 were only checked for finiteness): losses within 2e-3 relative, total gradient cosine
+    >= 0.995, norm within 1e-2.  Config 5's PV attention runs attention_flash_long.hip in bf16 and the exact-fp32
+    attention_long.hip in fp32.  Bars from the measured values (profiles/r5b_cfg_bf16_vs_fp32.txt: loss rel
+    <= 1.6e-4, cosine >= 0.9972, norm rel <= 2.8e-3), about 10x / 2x / 4x above them (round 4's 1e-2 / 0.99 / 5e-2
+    were the mixed-precision defaults)."""
     from golden_util import CFG_PATH
     from k3m_amd.config import pretrain_config
     from k3m_amd.engine import K3MEngine
@@ -83,8 +85,8 @@ def test_bf16_matches_fp32_step(dev, name):
     cos = float(gf @ gb / (gf.norm() * gb.norm()))
     nrel = abs(float(gb.norm()) - float(gf.norm())) / float(gf.norm())
     print("bf16 vs fp32 %s: loss rel" % name, rel, "grad cos %.6f norm rel %.3e" % (cos, nrel))
-    assert (rel <= 1e-2).all(), (lb, lf)
-    assert cos >= 0.99 and nrel <= 5e-2, (cos, nrel)
+    assert (rel <= 2e-3).all(), (lb, lf)
+    assert cos >= 0.995 and nrel <= 1e-2, (cos, nrel)
 
 
 # bs, T, P, boxes, triples, NPV per BASELINE.json configs

@@ -103,9 +103,12 @@ def test_train_mode_step_is_finite_and_learns(dev):
 # within BF16_GRAD_NORM_RTOL of the fp32 reference (small bias gradients that are sums of
 # cancelling terms carry the most relative bf16 noise, hence the per-tensor cosine bar), and all
 # recorded gradients together with cosine >= BF16_GLOBAL_COS.
-BF16_LOSS_RTOL = 1e-2
-BF16_GRAD_COS = 0.98
-BF16_GRAD_NORM_RTOL = 3e-2
+# Measured over the five goldens (round 5, profiles/r5c/bf16_golden_parity.txt): loss relative error <= 3.5e-3
+# (the NSP loss of bs3_zero_triple; the others <= 2.7e-3), worst per-tensor gradient cosine 0.9961, worst norm
+# relative 0.0096, global cosine >= 0.9973.  Bars about 2x above those (round 4: 1e-2 / 0.98 / 3e-2).
+BF16_LOSS_RTOL = 7e-3
+BF16_GRAD_COS = 0.99
+BF16_GRAD_NORM_RTOL = 2e-2
 BF16_GLOBAL_COS = 0.995
 # bf16 logit bars, set from the measured error distribution over the five goldens
 # (profiles/r4_bf16_logit_errors.json, scripts/bf16_logit_errors.py; error = |bf16 - ref| / row max |ref|):
