@@ -197,22 +197,25 @@ __global__ __launch_bounds__(FNT, 2) void flash_long_fwd_kernel(const uint16_t* 
 }
 
 // ------------------------------------------------------------------ backward
-// D[(s nh + h) lq + i] = dO_i . O_i over the head's dims (the bf16 O the forward wrote): 16 lanes per (row, head),
-// lane c loading the head's 16-B chunk c (hd / 8 <= 16 chunks), so a wave's loads are 4 whole head rows
+// D[(s nh + h) lq + i] = dO_i . O_i over the head's dims (the bf16 O the forward wrote): LPH lanes per (row, head)
+// (8 at d = 64, 16 at d = 96 / 128), lane c loading the head's 16-B chunk c, so a wave's loads are whole head rows
+// of consecutive heads.  32-bit index arithmetic (rows x heads < 2^31, checked by the caller): the 64-bit
+// divisions of the first form cost more than the loads (config 5: 145 us per launch for 252 MB).
+template <int LPH>
 __global__ __launch_bounds__(256) void flash_long_prep_kernel(const uint16_t* __restrict__ dctx, long long ldc,
                                                               const uint16_t* __restrict__ o, long long ldo,
                                                               float* __restrict__ dvec, int nseq, int lq, int nh,
                                                               int hd) {
-  const long long idx = ((long long)blockIdx.x * 256 + threadIdx.x) >> 4;   // (row, head)
-  const int c = threadIdx.x & 15;
-  const bool live = idx < (long long)nseq * lq * nh;
-  const long long id = live ? idx : 0;
-  const int h = (int)(id % nh);
-  const long long row = id / nh;   // sequence row s lq + i
+  const unsigned total = (unsigned)nseq * (unsigned)lq * (unsigned)nh;
+  const unsigned idx = (blockIdx.x * 256u + threadIdx.x) / LPH;   // (row, head)
+  const int c = threadIdx.x & (LPH - 1);
+  const bool live = idx < total;
+  const unsigned id = live ? idx : 0u;
+  const unsigned row = id / (unsigned)nh, h = id - row * (unsigned)nh;   // sequence row s lq + i
   float acc = 0.f;
   if (live && c < hd / 8) {
-    const uint4 a = *reinterpret_cast<const uint4*>(dctx + row * ldc + (long long)h * hd + 8 * c);
-    const uint4 b = *reinterpret_cast<const uint4*>(o + row * ldo + (long long)h * hd + 8 * c);
+    const uint4 a = *reinterpret_cast<const uint4*>(dctx + (long long)row * ldc + (long long)h * hd + 8 * c);
+    const uint4 b = *reinterpret_cast<const uint4*>(o + (long long)row * ldo + (long long)h * hd + 8 * c);
     const uint32_t wa[4] = {a.x, a.y, a.z, a.w}, wb[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -220,9 +223,9 @@ __global__ __launch_bounds__(256) void flash_long_prep_kernel(const uint16_t* __
              __uint_as_float(wa[t] & 0xffff0000u) * __uint_as_float(wb[t] & 0xffff0000u);
   }
 #pragma unroll
-  for (int m = 8; m > 0; m >>= 1) acc += __shfl_xor(acc, m, 64);
+  for (int m = LPH / 2; m > 0; m >>= 1) acc += __shfl_xor(acc, m, 64);
   if (live && c == 0) {
-    const int s = (int)(row / lq), i = (int)(row % lq);
+    const unsigned s = row / (unsigned)lq, i = row - s * (unsigned)lq;
     dvec[((long long)s * nh + h) * lq + i] = acc;
   }
 }
@@ -572,8 +575,13 @@ extern "C" int k3m_flash_attn_long_bwd(const void* dctx, long long ldc, const vo
   const long long rows = (long long)nseq * nh * lq;
   float* dvec = static_cast<float*>(ws);
   float* dq_ws = dvec + (rows + 63) / 64 * 64;
-  hipLaunchKernelGGL(flash_long_prep_kernel, dim3(k3m_cdiv(rows * 16, 256)), dim3(256), 0, st, (const uint16_t*)dctx, ldc,
-                     (const uint16_t*)o, ldo, dvec, nseq, lq, nh, hd);
+  K3M_ARG(rows * 16 < (1LL << 31));
+  if (hd == 64)
+    hipLaunchKernelGGL(flash_long_prep_kernel<8>, dim3(k3m_cdiv(rows * 8, 256)), dim3(256), 0, st,
+                       (const uint16_t*)dctx, ldc, (const uint16_t*)o, ldo, dvec, nseq, lq, nh, hd);
+  else
+    hipLaunchKernelGGL(flash_long_prep_kernel<16>, dim3(k3m_cdiv(rows * 16, 256)), dim3(256), 0, st,
+                       (const uint16_t*)dctx, ldc, (const uint16_t*)o, ldo, dvec, nseq, lq, nh, hd);
   const dim3 grid(nseq * nh, ngrp);
 #define K3M_FL_BWD(HD_)                                                                                          \
   hipLaunchKernelGGL(flash_long_bwd_kernel<HD_>, grid, dim3(64 * nw), lds, st, (const uint16_t*)dctx, ldc,        \
