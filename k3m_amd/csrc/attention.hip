@@ -637,7 +637,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_reg_kernel(const float* __res
             p4[b] = acc[kt][4 * a + b] * inv;
             acc[kt][4 * a + b] = j < lk ? p4[b] * k3m_drop(dr, off + prow + j) : 0.f;
           }
+#ifdef K3M_LAB_NO_PSTORE   // lab only (scripts/lab/lab_build.sh): the forward without its probability stores
+          if (false) {
+#else
           if (qok) {
+#endif
             if (vec && j0 < lk) {
               *reinterpret_cast<float4*>(probs + prow + j0) = make_float4(p4[0], p4[1], p4[2], p4[3]);
             } else if (!vec) {
@@ -899,7 +903,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x6_kernel(const float* __rest
             p4[b] = acc[kt][4 * a + b] * inv;
             acc[kt][4 * a + b] = j < lk ? p4[b] * k3m_drop(dr, off + prow + j) : 0.f;
           }
+#ifdef K3M_LAB_NO_PSTORE   // lab only (scripts/lab/lab_build.sh): the forward without its probability stores
+          if (false) {
+#else
           if (qok) {
+#endif
             if (vec && j0 < lk) {
               *reinterpret_cast<float4*>(probs + prow + j0) = make_float4(p4[0], p4[1], p4[2], p4[3]);
             } else if (!vec) {
