@@ -293,26 +293,36 @@ def deterministic():
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_deterministic_step_bit_identical(dev, dtype, deterministic):
+def test_deterministic_step_bit_identical(dev, dtype, deterministic, layout="default"):
     """K3M_DETERMINISTIC: with the fixed-order embedding / structure-aggregator / LPM backward the whole
     training step is bit-reproducible -- two trainers from the same state (dropout, device gumbel noise and
     device-drawn LPM negatives on) end bit-identical after three steps: parameters, both moments, the bf16 shadow.
     And the overlapped per-block AdamW (Trainer.overlap) equals the one sweep after the backward bit for bit over
-    the whole step, in both dtypes."""
+    the whole step, in both dtypes.  layout (test_deterministic_overlap_layouts): the config-5
+    shapes (PV 320 on the long-attention kernels, 50 triples) and the reference's pretrained-model parameter groups
+    (per-tensor lr multipliers, frozen embeddings and first text layers: train_concap_struc.py:255-257, :352-389),
+    where a block released to the side-stream AdamW before its backward finished would show."""
     from k3m_amd.trainer import Trainer
     from k3m_amd.synthetic import synthetic_batch
     from k3m_amd.config import pretrain_config
     from k3m_amd.engine import label_counts
     cfg = pretrain_config(CFG_PATH)
-    B = 4
+    B = 4 if layout != "cfg5" else 2
+    shape = dict(n_triples=6) if layout != "cfg5" else dict(P=320, n_triples=50, npv=50)
     batches = []
     for s in (61, 62, 63):
-        b = synthetic_batch(cfg, B, dev, seed=s, n_triples=6)
+        b = synthetic_batch(cfg, B, dev, seed=s, **shape)
         b["_label_counts"] = label_counts(b)
         batches.append(b)
+    kw = {}
+    if layout == "groups":
+        from k3m_amd.params import flat_layout
+        names = [n for n, _ in flat_layout(cfg)[0]]
+        kw["frozen_names"] = tuple(n for n in names if n.startswith("embeddings.") or n.startswith("encoder.layer.0."))
+        kw["lr_mult"] = {n: 0.1 for n in names if n.startswith("encoder.layer.") and n not in kw["frozen_names"]}
 
     def run(overlap):
-        tr = Trainer(cfg, dev, lr=1e-3, warmup_steps=1, total_steps=10, seed=11, dtype=dtype)
+        tr = Trainer(cfg, dev, lr=1e-3, warmup_steps=1, total_steps=10, seed=11, dtype=dtype, **kw)
         tr.overlap = overlap
         tr.graph = False
         assert tr.dropout
@@ -327,6 +337,12 @@ def test_deterministic_step_bit_identical(dev, dtype, deterministic):
             continue
         assert torch.equal(x, y)   # run to run
         assert torch.equal(x, z)   # overlapped AdamW == the sweep, over the whole step
+
+
+@pytest.mark.parametrize("layout", ["cfg5", "groups"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_deterministic_overlap_layouts(dev, dtype, deterministic, layout):
+    test_deterministic_step_bit_identical(dev, dtype, deterministic, layout)
 
 
 def test_deterministic_gradients_match_atomic_form(dev):
