@@ -24,6 +24,7 @@ per-task losses), which outlive the next replay; larger outputs (logit-sized ten
 tensors, overwritten by the next replay (clone what must outlive it).  A capture that fails (an op that
 cannot be captured, a host sync on an untested path) is dropped with a warning and that key runs eagerly.
 """
+import gc
 import warnings
 
 import numpy as np
@@ -112,10 +113,18 @@ class StepGraph(object):
         eng.graph_seed = self.seed.data_ptr()
         eng.capturing = True
         tr._adam_table = self.table
+        # no automatic garbage collection while the stream captures: a collected cycle holding a HIP object (an
+        # event of an earlier trainer, a stream) would run its destructor mid-capture, where HIP refuses the call
+        # and the C++ destructor aborts the process (seen once in the full GPU suite, test_gpu_graph)
+        gc.collect()
+        gc_was = gc.isenabled()
+        gc.disable()
         try:
             with torch.cuda.graph(self.graph, capture_error_mode="relaxed"):
                 self.out = tr._device_step(self.static)
         finally:
+            if gc_was:
+                gc.enable()
             eng.graph_seed = 0
             eng.capturing = False
             tr._adam_table = None
