@@ -194,7 +194,229 @@ struct Loop {
   }
 };
 
-template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, int EPI, bool PIPE>
+// ---------------------------------------------------------------------------------------------------
+// Ping-pong main loop (K3M_X6_PP).  The two waves that share a SIMD (w and w + 4) run the same k-loop
+// one phase apart, so that one wave's MFMAs run while its partner reads fragments, splits and writes the
+// next k-tile and issues the global loads:
+//
+//   phase      0        1        2        3      ...
+//   waves 0-3  M(0)     C(0)     M(1)     C(1)
+//   waves 4-7  (wait)   M(0)     C(0)     M(1)
+//
+// M(t): read this wave's fragments of k-tile t (stage t&1) into registers; split this wave GROUP's half
+//       of k-tile t+1 (loaded one iteration earlier) into stage (t+1)&1; load its half of k-tile t+2.
+// C(t): the 6 (x BK/16) MFMAs per accumulator, registers only.
+// One s_barrier ends every phase.  Stage (t+1)&1 is written in phases 2t (waves 0-3) and 2t+1 (waves
+// 4-7) and first read in phase 2t+2; its previous k-tile t-1 was last read in phase 2t-1.  Each group
+// stages half of every operand tile (rows [0, TILE/2) by waves 0-3, [TILE/2, TILE) by waves 4-7), one
+// register set per thread (loads have two phases to land).  Waves 4-7 enter one barrier late and waves
+// 0-3 leave one barrier late, so both execute 2 nt + 2 barriers per tile.
+// In round 5's compiler-scheduled loop both waves of a SIMD reached the barrier, the fragment-read
+// burst and the MFMAs together (MFMA busy 0.58 of the cycles, 55 % of wave cycles in WAIT_INST_ANY).
+template <bool KC, int TILE, int BK>
+struct PPHalf {
+  static constexpr int NTG = 256;               // threads per wave group
+  static constexpr int HT = TILE / 2;           // mn rows / columns staged by one group
+  static constexpr int NV = HT * BK / 4;        // float4 per half tile
+  static constexpr int NB = NV / NTG;
+  static_assert(NV % NTG == 0, "half tile must be a whole number of float4 per thread");
+  floatx4 r[NB];
+  const float* p[NB];
+  int kq[NB];
+
+  __device__ __forceinline__ void init(const float* __restrict__ base, long long ld, int mn0, int kbeg, int MN, int t,
+                                       int half) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int idx = t + NTG * b;
+      if constexpr (KC) {
+        const int row = half * HT + idx / (BK / 4), q = idx % (BK / 4);
+        kq[b] = 4 * q;
+        p[b] = base + (long long)min(mn0 + row, MN - 1) * ld + kbeg + 4 * q;
+      } else {
+        const int col = half * HT + 4 * (idx % (HT / 4)), kr = idx / (HT / 4);
+        kq[b] = kr;
+        p[b] = base + (long long)(kbeg + kr) * ld + max(0, min(mn0 + col, MN - 4));
+      }
+    }
+  }
+  // load the k-tile at the pointers and advance them.  krem < BK: a partial last tile; its lanes past
+  // krem read the tile's first k (a valid address) and keep zeros, without exec-masked branches
+  __device__ __forceinline__ void load(long long ld, int krem) {
+    if (krem >= BK) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        r[b] = *reinterpret_cast<const floatx4*>(p[b]);
+        p[b] += KC ? BK : BK * ld;
+      }
+    } else {
+      const floatx4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const bool in = kq[b] < krem;
+        const float* q = in ? p[b] : p[b] - (KC ? kq[b] : (long long)kq[b] * ld);
+        const floatx4 v = *reinterpret_cast<const floatx4*>(q);
+        r[b] = in ? v : z;
+        p[b] += KC ? BK : BK * ld;
+      }
+    }
+  }
+  // split + write the half tile into the three planes of one operand image (plane stride TILE * BK)
+  __device__ __forceinline__ void store(__bf16* __restrict__ lds, int t, int half) const {
+    constexpr int PL = TILE * BK;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int idx = t + NTG * b;
+      int off;
+      if constexpr (KC) {
+        const int row = half * HT + idx / (BK / 4), q = idx % (BK / 4);
+        off = slot_off<BK>(row, q >> 1) + 4 * (q & 1);
+      } else {
+        const int c4 = half * (HT / 4) + idx % (HT / 4), kr = idx / (HT / 4);
+        off = mn_off<TILE>(kr, c4 >> 1) + 4 * (c4 & 1);
+      }
+      u32x2v h, m, l;
+      split4(r[b], h, m, l);
+      *reinterpret_cast<u32x2v*>(lds + off) = h;
+      *reinterpret_cast<u32x2v*>(lds + PL + off) = m;
+      *reinterpret_cast<u32x2v*>(lds + 2 * PL + off) = l;
+    }
+  }
+};
+
+// s_waitcnt lgkmcnt(0) (vmcnt / expcnt left at their maxima) + s_barrier, pinned in program order
+__device__ __forceinline__ void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_>
+struct PPLoop {
+  static_assert(WM * WN == 8, "ping-pong pairs waves w and w + 4 of an 8-wave workgroup");
+  static constexpr int FM = TBM / WM / 32, FN = TBN / WN / 32, KS = BK / 16;
+  static constexpr int BUF = 3 * (TBM + TBN) * BK;
+  static constexpr int PA = TBM * BK, PB = TBN * BK;
+  PPHalf<AK, TBM, BK> ha;
+  PPHalf<BK_, TBN, BK> hb;
+  long long lda, ldb;
+  int nt, krem;   // k-tiles (the last one partial when krem > 0), k values of the partial tile
+
+  __device__ __forceinline__ int tile_k(int t) const { return (krem > 0 && t == nt - 1) ? krem : BK; }
+
+  __device__ __forceinline__ void prefetch(const K3mGemm& g, const Unit& u) {
+    const int t = threadIdx.x & 255, half = threadIdx.x >> 8;
+    lda = g.lda;
+    ldb = g.ldb;
+    ha.init(static_cast<const float*>(g.a), lda, u.m0, u.kbeg, g.m, t, half);
+    hb.init(static_cast<const float*>(g.b), ldb, u.n0, u.kbeg, g.n, t, half);
+    const int klen = u.kend - u.kbeg;
+    const int nkf = klen > 0 ? klen / BK : 0;
+    krem = klen > 0 ? klen - nkf * BK : 0;
+    nt = nkf + (krem > 0 ? 1 : 0);
+    if (nt > 0) {
+      const int kk = tile_k(0);
+      ha.load(lda, kk);
+      hb.load(ldb, kk);
+    }
+  }
+  __device__ __forceinline__ void prefetch2() {}
+
+  __device__ __forceinline__ void frags(const __bf16* stage, bf16x8 (&a)[KS][3][FM], bf16x8 (&b)[KS][3][FN]) const {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wm = (w / WN) * (TBM / WM), wn = (w % WN) * (TBN / WN);
+    const int h = lane >> 5, cl = lane & 31;
+    const __bf16* as = stage;
+    const __bf16* bs = as + 3 * PA;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          a[ks][pl][i] = AK ? *reinterpret_cast<const bf16x8*>(as + pl * PA + slot_off<BK>(wm + 32 * i + cl, 2 * ks + h))
+                            : mn_frag<TBM>(as + pl * PA, wm + 32 * i, ks, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          b[ks][pl][j] = BK_ ? *reinterpret_cast<const bf16x8*>(bs + pl * PB + slot_off<BK>(wn + 32 * j + cl, 2 * ks + h))
+                             : mn_frag<TBN>(bs + pl * PB, wn + 32 * j, ks, lane);
+      }
+  }
+
+  __device__ __forceinline__ static void mfma(const bf16x8 (&a)[KS][3][FM], const bf16x8 (&b)[KS][3][FN],
+                                              floatx16 (&acc)[FM][FN]) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          // smallest terms first: (hl + mm + lh), (hm + mh), hh -- the order of Loop::compute
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][0][i], b[ks][2][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][1][i], b[ks][1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][2][i], b[ks][0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][0][i], b[ks][1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][1][i], b[ks][0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][0][i], b[ks][0][j], acc[i][j], 0, 0, 0);
+        }
+  }
+
+  __device__ __forceinline__ void stage_half(__bf16* stage) const {
+    const int t = threadIdx.x & 255, half = threadIdx.x >> 8;
+    ha.store(stage, t, half);
+    hb.store(stage + 3 * PA, t, half);
+  }
+
+  // Same contract as Loop::run.
+  __device__ __forceinline__ void run(__bf16* smem, floatx16 (&acc)[FM][FN]) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const bool late = threadIdx.x >= 256;   // waves 4-7
+    if (nt > 0) {
+      stage_half(smem);
+      if (nt > 1) {
+        const int kk = tile_k(1);
+        ha.load(lda, kk);
+        hb.load(ldb, kk);
+      }
+    }
+    pp_barrier();
+    if (late) pp_barrier();
+    for (int kt = 0; kt < nt; ++kt) {
+      const int cur = kt & 1;
+      bf16x8 a[KS][3][FM], b[KS][3][FN];
+      frags(smem + cur * BUF, a, b);
+      if (kt + 1 < nt) {
+        stage_half(smem + (cur ^ 1) * BUF);
+        if (kt + 2 < nt) {
+          const int kk = tile_k(kt + 2);
+          ha.load(lda, kk);
+          hb.load(ldb, kk);
+        }
+      }
+      pp_barrier();
+      mfma(a, b, acc);
+      pp_barrier();
+    }
+    if (!late) pp_barrier();
+  }
+};
+
+template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool PIPE, bool PP>
+struct LoopSel {
+  using T = Loop<TBM, TBN, WM, WN, BK, AK, BK_, PIPE>;
+};
+template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool PIPE>
+struct LoopSel<TBM, TBN, WM, WN, BK, AK, BK_, PIPE, true> {
+  using T = PPLoop<TBM, TBN, WM, WN, BK, AK, BK_>;
+};
+
+template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, int EPI, bool PIPE, bool PP = false>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_x6_persist_kernel(GemmGroup grp) {
   constexpr int LDS_BF16 = 2 * 3 * (TBM + TBN) * BK;
   constexpr int EPI_F32 = WM * WN * 32 * (TBN / WN + 8);
@@ -203,7 +425,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_x6_persist_kernel(GemmGr
   const int total = grp.start[grp.count];
   int u = blockIdx.x;
   if (u >= total) return;
-  Loop<TBM, TBN, WM, WN, BK, AK, BK_, PIPE> lp;
+  typename LoopSel<TBM, TBN, WM, WN, BK, AK, BK_, PIPE, PP>::T lp;
   Unit cur = decode<TBM, TBN, BK>(grp, u);
   lp.prefetch(grp.g[cur.p], cur);
   lp.prefetch2();
@@ -227,13 +449,13 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_x6_persist_kernel(GemmGr
   }
 }
 
-template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool PIPE>
+template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool PIPE, bool PP = false>
 int launch(const GemmGroup& grp, int epi, int nblk, hipStream_t st) {
   const dim3 grid(nblk);
   switch (epi) {
 #define K3M_P_CASE(E)                                                                                       \
     case E:                                                                                                 \
-      hipLaunchKernelGGL((gemm_x6_persist_kernel<TBM, TBN, WM, WN, BK, AK, BK_, E, PIPE>), grid,            \
+      hipLaunchKernelGGL((gemm_x6_persist_kernel<TBM, TBN, WM, WN, BK, AK, BK_, E, PIPE, PP>), grid,        \
                          dim3(64 * WM * WN), 0, st, grp);                                                   \
       break;
     K3M_P_CASE(K3M_EPI_NONE)
@@ -248,6 +470,11 @@ int launch(const GemmGroup& grp, int epi, int nblk, hipStream_t st) {
   return 0;
 }
 
+// K3M_X6_PP: ping-pong main loop (PPLoop) per operand-layout class, bitmask as K3M_X6_TILE256: 1 forward
+// (both K-contiguous), 2 input gradient (B MN-contiguous), 4 weight gradient (both MN-contiguous),
+// 8 A MN-contiguous / B K-contiguous; 16 = the 256x128 tiles too.
+const int kPP = k3m_env_int("K3M_X6_PP", 0);
+
 }  // namespace
 }  // namespace k3m_x6
 
@@ -259,16 +486,25 @@ int k3m_x6_persistent_launch(const k3m_x6::GemmGroup& grp, bool t256, bool ak, b
   const int nblk = total < cus ? total : cus;
   const int epi = grp.g[0].epilogue;
   using namespace k3m_x6;
+  const int cls = ak && bk ? 1 : ak ? 2 : !bk ? 4 : 8;
+  const bool pp = (kPP & cls) != 0 && (t256 || (kPP & 16) != 0);
   if (t256) {
-    if (ak && bk) return launch<256, 256, 4, 2, 16, true, true, true>(grp, epi, nblk, st);
-    if (ak) return launch<256, 256, 2, 4, 16, true, false, true>(grp, epi, nblk, st);
-    if (!bk) return launch<256, 256, 2, 4, 16, false, false, false>(grp, epi, nblk, st);
+    if (ak && bk) return pp ? launch<256, 256, 4, 2, 16, true, true, true, true>(grp, epi, nblk, st)
+                            : launch<256, 256, 4, 2, 16, true, true, true>(grp, epi, nblk, st);
+    if (ak) return pp ? launch<256, 256, 2, 4, 16, true, false, true, true>(grp, epi, nblk, st)
+                      : launch<256, 256, 2, 4, 16, true, false, true>(grp, epi, nblk, st);
+    if (!bk) return pp ? launch<256, 256, 2, 4, 16, false, false, false, true>(grp, epi, nblk, st)
+                       : launch<256, 256, 2, 4, 16, false, false, false>(grp, epi, nblk, st);
     return K3M_EINVAL;
   }
-  if (ak && bk) return launch<256, 128, 4, 2, 32, true, true, true>(grp, epi, nblk, st);
-  if (ak) return launch<256, 128, 4, 2, 32, true, false, true>(grp, epi, nblk, st);
-  if (bk) return launch<256, 128, 4, 2, 32, false, true, true>(grp, epi, nblk, st);
-  return launch<256, 128, 4, 2, 32, false, false, false>(grp, epi, nblk, st);
+  if (ak && bk) return pp ? launch<256, 128, 4, 2, 32, true, true, true, true>(grp, epi, nblk, st)
+                          : launch<256, 128, 4, 2, 32, true, true, true>(grp, epi, nblk, st);
+  if (ak) return pp ? launch<256, 128, 4, 2, 32, true, false, true, true>(grp, epi, nblk, st)
+                    : launch<256, 128, 4, 2, 32, true, false, true>(grp, epi, nblk, st);
+  if (bk) return pp ? launch<256, 128, 4, 2, 32, false, true, true, true>(grp, epi, nblk, st)
+                    : launch<256, 128, 4, 2, 32, false, true, true>(grp, epi, nblk, st);
+  return pp ? launch<256, 128, 4, 2, 32, false, false, false, true>(grp, epi, nblk, st)
+            : launch<256, 128, 4, 2, 32, false, false, false>(grp, epi, nblk, st);
 }
 
 // Two-workgroups-per-CU variant (A/B knob K3M_X6_VARIANT=1 in gemm.hip): 128x256x16 tiles of 4 waves (each

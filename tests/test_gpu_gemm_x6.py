@@ -195,6 +195,15 @@ out["t128"] = ops.linear(x2, w2, b2)
 with ops.grouped():
     g1 = ops.linear(x2, w2, b2); g2 = ops.linear(x[:2304], w[:1024], b[:1024])
 out["g1"], out["g2"] = g1, g2
+# k not a multiple of the k-tile (a partial last k-tile on every layout), and a split-K slice edge
+x3 = torch.randn(3000, 1000, device=dev); w3 = torch.randn(2304, 1000, device=dev) * 0.05
+out["ktail_fwd"] = ops.linear(x3, w3, None)
+dy3 = torch.randn(3000, 2304, device=dev)
+out["ktail_dgrad"] = ops.linear_dgrad(dy3, w3)
+gw3 = torch.zeros(2304, 1000, device=dev)
+ops.linear_wgrad(dy3[:2996], x3[:2996], gw3); out["ktail_wgrad"] = gw3
+x4 = torch.randn(2500, 776, device=dev); w4 = torch.randn(1024, 776, device=dev) * 0.05
+out["ktail_t128"] = ops.linear(x4, w4, None)
 torch.cuda.synchronize()
 torch.save({k: v.cpu() for k, v in out.items()}, sys.argv[1])
 '''
@@ -203,7 +212,9 @@ torch.save({k: v.cpu() for k, v in out.items()}, sys.argv[1])
 def test_persistent_walk_bit_identical(tmp_path):
     """The persistent x6 walk (gemm_x6p.hip, K3M_X6_PERSIST=1, default) computes every tile exactly as the
     one-workgroup-per-tile kernels (K3M_X6_PERSIST=0): bit-identical C, aux, split-K sums and grouped
-    outputs (the knob is read at library load, so each setting runs in its own process)."""
+    outputs, and so do the persistent walks with the ping-pong main loop (K3M_X6_PP=31, every layout and tile)
+    and with it off (K3M_X6_PP=0).  The knobs are read at library load, so each setting runs in its own
+    process."""
     import os
     import subprocess
     import sys
@@ -211,13 +222,15 @@ def test_persistent_walk_bit_identical(tmp_path):
     script = tmp_path / "persist_case.py"
     script.write_text(_PERSIST_SCRIPT)
     res = {}
-    for knob in ("0", "1"):
-        path = str(tmp_path / ("out%s.pt" % knob))
-        env = dict(os.environ, K3M_X6_PERSIST=knob)
+    for name, knobs in (("tile", {"K3M_X6_PERSIST": "0"}), ("walk", {"K3M_X6_PERSIST": "1", "K3M_X6_PP": "0"}),
+                        ("pp", {"K3M_X6_PERSIST": "1", "K3M_X6_PP": "31"})):
+        path = str(tmp_path / ("out_%s.pt" % name))
+        env = dict(os.environ, **knobs)
         subprocess.run([sys.executable, str(script), path, repo], check=True, env=env, timeout=240)
-        res[knob] = torch.load(path, weights_only=True)
-    for k in res["0"]:
-        assert torch.equal(res["0"][k], res["1"][k]), k
+        res[name] = torch.load(path, weights_only=True)
+    for name in ("walk", "pp"):
+        for k in res["tile"]:
+            assert torch.equal(res["tile"][k], res[name][k]), (name, k)
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
