@@ -334,6 +334,161 @@ __device__ __forceinline__ void mainloop32(const uint16_t* __restrict__ A, long 
   __syncthreads();
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Ping-pong main loop (K3M_B16_PP): the two waves of each SIMD (w and w + 4) run one phase apart, one
+// issuing MFMAs while the other reads its fragments (same rationale and phase table as PPLoop in
+// gemm_x6p.hip).  Per k-tile t (64 deep, stage t & 1), waves 0-3 run M(t) in phase 2t and C(t) in 2t+1,
+// waves 4-7 one phase later.  M(t): all fragments of k-tile t into registers.  C(t): the k-tile's MFMAs.
+// LDS-DMA: both groups issue their half of k-tile t+2 into stage t & 1 in phase 2t+2 (waves 0-3 at the
+// head of M(t+1), waves 4-7 at the head of C(t)), after the last read of k-tile t (phase 2t+1), and
+// both wait for it (vmcnt(0)) at the end of phase 2t+3, before its first read in phase 2t+4.
+template <bool KC, int TILE>
+struct HalfLoader {   // the DMA instructions of one half of an operand tile, spread over 4 waves
+  static constexpr int INSTS = TILE * BK * 2 / 1024;
+  static constexpr int NI = INSTS / 8;   // per wave
+  static_assert(INSTS % 8 == 0, "half tile must split evenly over 4 waves");
+  const uint16_t* base;
+  long long step;
+  uint32_t off[NI];
+  int lds0;
+
+  __device__ __forceinline__ void init(const uint16_t* __restrict__ a, long long ld, int mn0, int kbeg, int MN) {
+    const int l = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int first = (w >> 2) * (INSTS / 2) + (w & 3);   // instruction i of this wave: first + 4 i
+    lds0 = first * 512;
+    base = a + (KC ? (long long)kbeg : (long long)kbeg * ld);
+    step = KC ? BK : BK * ld;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int inst = first + 4 * i;
+      if constexpr (KC) {
+        const int row = inst * 8 + (l >> 3), slot = l & 7;
+        const int ch = slot ^ ((row >> 1) & 7);
+        off[i] = (uint32_t)((long long)min(mn0 + row, MN - 1) * ld + ch * 8);
+      } else {
+        constexpr int CPR = TILE / 8, RPI = 64 / CPR;
+        const int kr = inst * RPI + l / CPR, slot = l % CPR;
+        const int ch = slot ^ (((kr & 3) << 2) | ((kr >> 2) & 3));
+        off[i] = (uint32_t)((long long)kr * ld + max(0, min(mn0 + ch * 8, MN - 8)));
+      }
+    }
+  }
+  __device__ __forceinline__ void issue(uint16_t* img) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) glds16(base + off[i], img + lds0 + i * 4 * 512);
+    base += step;
+  }
+};
+
+__device__ __forceinline__ void pp_sync(bool vm) {
+  __builtin_amdgcn_sched_barrier(0);
+  if (vm) __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0)
+  else __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// PH > 1 cuts each k-tile into PH M/C phase pairs of SUB / PH substeps (the 256 x 256 tile: 96 fragment
+// registers of a whole k-tile beside 128 accumulators spill); the DMA rules hold per k-tile: waves 0-3 issue
+// in the first M phase of k-tile kt and wait at the end of its last C phase, waves 4-7 issue in the last C
+// phase of k-tile kt and wait at the end of the last M phase of k-tile kt + 1.
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int MF>
+__device__ __forceinline__ void mainloop_pp(const uint16_t* __restrict__ A, long long lda,
+                                            const uint16_t* __restrict__ B, long long ldb, int M, int N, int m0,
+                                            int n0, int kbeg, int kend, uint16_t* smem,
+                                            Acc<MF, TBM / WM, TBN / WN>& accs) {
+  static_assert(WM * WN == 8, "ping-pong pairs waves w and w + 4");
+  using S = Shape<TBM, TBN, WM, WN>;
+  constexpr int FM = TBM / WM / MF, FN = TBN / WN / MF;
+  constexpr int SUB = MF == 16 ? BK / 32 : BK / 16;   // k-substeps per k-tile
+  constexpr int PH = (TBM / WM) * (TBN / WN) >= 128 * 64 ? 2 : 1;
+  constexpr int SP = SUB / PH;                         // substeps per phase
+  auto& acc = accs.v;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = (w / WN) * (TBM / WM), wn = (w % WN) * (TBN / WN);
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      if constexpr (MF == 16) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      else
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    }
+  HalfLoader<AK, TBM> la;
+  HalfLoader<BK_, TBN> lb;
+  la.init(A, lda, m0, kbeg, M);
+  lb.init(B, ldb, n0, kbeg, N);
+  const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
+  if (nk == 0) return;
+  const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8) != 0;   // waves 4-7
+  la.issue(smem);
+  lb.issue(smem + TBM * BK);
+  if (nk > 1) {
+    la.issue(smem + S::STAGE);
+    lb.issue(smem + S::STAGE + TBM * BK);
+  }
+  pp_sync(true);
+  if (late) pp_sync(false);
+  bf16x8 a[SP][FM], b[SP][FN];
+  auto rd = [&](const uint16_t* st, int ph) {
+#pragma unroll
+    for (int q = 0; q < SP; ++q) {
+      const int s = ph * SP + q;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        a[q][i] = MF == 16 ? frag<AK, TBM>(st, wm + 16 * i, s, lane) : frag32<AK, TBM>(st, wm + 32 * i, s, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        b[q][j] = MF == 16 ? frag<BK_, TBN>(st + TBM * BK, wn + 16 * j, s, lane)
+                           : frag32<BK_, TBN>(st + TBM * BK, wn + 32 * j, s, lane);
+    }
+  };
+  auto mm = [&]() {
+#pragma unroll
+    for (int q = 0; q < SP; ++q)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          if constexpr (MF == 16) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[q][i], b[q][j], acc[i][j], 0, 0, 0);
+          else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q][i], b[q][j], acc[i][j], 0, 0, 0);
+        }
+  };
+#pragma nounroll
+  for (int kt = 0; kt < nk; ++kt) {
+    uint16_t* cur = smem + (kt & 1) * S::STAGE;
+    if (!late) {
+#pragma unroll
+      for (int ph = 0; ph < PH; ++ph) {
+        if (ph == 0 && kt >= 1 && kt + 1 < nk) {   // k-tile kt+1 into the stage k-tile kt-1 left
+          uint16_t* nxt = smem + ((kt + 1) & 1) * S::STAGE;
+          la.issue(nxt);
+          lb.issue(nxt + TBM * BK);
+        }
+        rd(cur, ph);
+        pp_sync(false);
+        mm();
+        pp_sync(ph == PH - 1);
+      }
+    } else {
+#pragma unroll
+      for (int ph = 0; ph < PH; ++ph) {
+        rd(cur, ph);
+        pp_sync(ph == PH - 1);
+        if (ph == PH - 1 && kt + 2 < nk) {         // k-tile kt+2 into the stage just read
+          la.issue(cur);
+          lb.issue(cur + TBM * BK);
+        }
+        mm();
+        pp_sync(false);
+      }
+    }
+  }
+  if (!late) pp_sync(false);
+}
+
 __device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
   const floatx4 a = *reinterpret_cast<const floatx4*>(p), b = *reinterpret_cast<const floatx4*>(p + 4);
   v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
@@ -679,7 +834,7 @@ struct PUnit {
   }
 };
 
-template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF, bool PRE>
+template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF, bool PRE, bool PP = false>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_persist_kernel(GemmGroup grp) {
   using S = Shape<TBM, TBN, WM, WN>;
   constexpr int EOFF = PRE ? TBM * BK + TBN * BK : 0;   // the epilogue image after stage 0 when prefetching
@@ -700,7 +855,11 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_persist_kernel(GemmGroup
   for (;;) {   // uniform over the workgroup: every wave leaves together
     const K3mGemm& g = grp.g[cur.p];
     Acc<MF, TBM / WM, TBN / WN> acc;
-    if constexpr (MF == 32)
+    if constexpr (PP && !PRE)
+      mainloop_pp<TBM, TBN, WM, WN, AK, BK_, MF>(static_cast<const uint16_t*>(g.a), g.lda,
+                                                 static_cast<const uint16_t*>(g.b), g.ldb, g.m, g.n, cur.m0, cur.n0,
+                                                 cur.kbeg, cur.kend, smem, acc);
+    else if constexpr (MF == 32)
       mainloop32<TBM, TBN, WM, WN, AK, BK_>(static_cast<const uint16_t*>(g.a), g.lda, static_cast<const uint16_t*>(g.b),
                                             g.ldb, g.m, g.n, cur.m0, cur.n0, cur.kbeg, cur.kend, smem, acc, pre);
     else

@@ -486,6 +486,11 @@ const int kB16Stagger = k3m_env_int("K3M_B16_STAGGER", 500);
 // other's MFMAs (FFN1 fwd -2 %, FFN2 dgrad+dGELU -4 %, co-attention PV FFN1 -14 %), while the plain main loop
 // is 10-25 % slower at 256 x 128 x 32 (1.5x the operand bytes per MFMA of 256 x 256; profiles/r4b_ab_dual.txt)
 const int kB16Dual = k3m_env_int("K3M_B16_DUAL", 2);
+// K3M_B16_PP: the persistent walk with the ping-pong main loop (mainloop_pp, gemm_b16_tile.h), bit 0 for the
+// v_mfma_f32_16x16x32 layouts (both operands K-contiguous), bit 1 for the 32x32x16 ones (MN-contiguous B); the
+// 256 x 128 tiles only unless bit 2 is set (the 256 x 256 ping-pong loop spills its fragment addresses)
+// measured slower on config 3 (profiles/r5d/README.txt): off
+const int kB16PP = k3m_env_int("K3M_B16_PP", 0);
 constexpr bool dual_epi(int epi) { return epi == K3M_EPI_BIAS_GELU || epi == K3M_EPI_DGELU; }
 
 long long nb_of(const K3mGemm& g, int bm, int bn);
@@ -515,7 +520,10 @@ void persist_launch(const k3m_b16::GemmGroup& grp_in, hipStream_t st) {
   grp.stagger = kB16Stagger;
   const int total = grp.start[grp.count];
   const int nblk = total < b16_cus() ? total : b16_cus();
-  if (kB16Prefetch)
+  if ((kB16PP & (MF == 16 ? 1 : 2)) != 0 && (TBN == 128 || (kB16PP & 4) != 0))
+    hipLaunchKernelGGL((k3m_b16::gemm_persist_kernel<TBM, TBN, WM, WN, AK, BK_, EPI, CT, MF, false, true>), dim3(nblk),
+                       dim3(64 * WM * WN), 0, st, grp);
+  else if (kB16Prefetch)
     hipLaunchKernelGGL((k3m_b16::gemm_persist_kernel<TBM, TBN, WM, WN, AK, BK_, EPI, CT, MF, true>), dim3(nblk),
                        dim3(64 * WM * WN), 0, st, grp);
   else

@@ -470,10 +470,14 @@ int launch(const GemmGroup& grp, int epi, int nblk, hipStream_t st) {
   return 0;
 }
 
-// K3M_X6_PP: ping-pong main loop (PPLoop) per operand-layout class, bitmask as K3M_X6_TILE256: 1 forward
-// (both K-contiguous), 2 input gradient (B MN-contiguous), 4 weight gradient (both MN-contiguous),
-// 8 A MN-contiguous / B K-contiguous; 16 = the 256x128 tiles too.
-const int kPP = k3m_env_int("K3M_X6_PP", 0);
+// K3M_X6_PP: ping-pong main loop (PPLoop) per operand-layout class, bitmask: 1 forward (both K-contiguous),
+// 2 input gradient (B MN-contiguous), 4 weight gradient (both MN-contiguous), 8 A MN-contiguous / B
+// K-contiguous; 16 = the 256x128 tiles too; 32 = the 256x256 weight-gradient walk too.  Default 31: same box,
+// interleaved (profiles/r5d/ab_x6_pp_gemm_shapes.txt) the K-contiguous 256x256 forwards / input gradients 4-7 % faster
+// (FFN2 0.460 -> 0.430 ms), the 256x128 and image / co-attention shapes 5-15 %, the dGELU input gradient
+// equal, but the 256x256 weight-gradient walk (both operands streamed from HBM, K = 20,992) 22-27 % SLOWER:
+// its loads get two phases (one k-tile of the faster loop) to land and do not.
+const int kPP = k3m_env_int("K3M_X6_PP", 31);
 
 }  // namespace
 }  // namespace k3m_x6
@@ -487,7 +491,7 @@ int k3m_x6_persistent_launch(const k3m_x6::GemmGroup& grp, bool t256, bool ak, b
   const int epi = grp.g[0].epilogue;
   using namespace k3m_x6;
   const int cls = ak && bk ? 1 : ak ? 2 : !bk ? 4 : 8;
-  const bool pp = (kPP & cls) != 0 && (t256 || (kPP & 16) != 0);
+  const bool pp = (kPP & cls) != 0 && (t256 ? (cls != 4 || (kPP & 32) != 0) : (kPP & 16) != 0);
   if (t256) {
     if (ak && bk) return pp ? launch<256, 256, 4, 2, 16, true, true, true, true>(grp, epi, nblk, st)
                             : launch<256, 256, 4, 2, 16, true, true, true>(grp, epi, nblk, st);

@@ -288,3 +288,58 @@ def test_flash_long_backward_deterministic(dev, lq, lk, nh, hd):
     for a, b in zip(*outs):
         assert torch.isfinite(a.float()).all()
         assert torch.equal(a, b)
+
+
+_B16_WALK_SCRIPT = r'''
+import sys, torch
+sys.path.insert(0, sys.argv[2])
+from k3m_amd import ops, _lib as L
+dev = torch.device("cuda")
+out = {}
+torch.manual_seed(7)
+bf = torch.bfloat16
+# 256x256 and 256x128 forwards (bias, bias+GELU, ragged M), input gradients with and without dGELU, split-K
+# weight gradients and a grouped launch, all in bf16 (the persistent walk's layouts and both MFMA shapes)
+x = torch.randn(5000, 768, device=dev).to(bf); w = (torch.randn(3072, 768, device=dev) * 0.05).to(bf)
+b = torch.randn(3072, device=dev)
+pre = torch.empty(5000, 3072, device=dev, dtype=bf)
+out["fwd_gelu"] = ops.linear(x, w, b, epi=L.EPI_BIAS_GELU, aux=pre); out["pre"] = pre
+out["fwd_bias"] = ops.linear(x, w, b)
+x2 = torch.randn(2368, 1024, device=dev).to(bf); w2 = (torch.randn(1024, 1024, device=dev) * 0.05).to(bf)
+out["fwd_t128"] = ops.linear(x2, w2, b[:1024])
+dy = torch.randn(5000, 3072, device=dev).to(bf); aux = torch.randn(5000, 768, device=dev).to(bf)
+out["dgrad_dgelu"] = ops.linear_dgrad(dy, w, dgelu_aux=aux)
+out["dgrad"] = ops.linear_dgrad(dy, w)
+gw = torch.ones(3072, 768, device=dev)
+ops.linear_wgrad(dy, x, gw); out["wgrad"] = gw
+with ops.grouped():
+    g1 = ops.linear(x2, w2, b[:1024]); g2 = ops.linear(x[:2304], w[:1024], b[:1024])
+out["g1"], out["g2"] = g1, g2
+torch.cuda.synchronize()
+torch.save({k: v.float().cpu() for k, v in out.items()}, sys.argv[1])
+'''
+
+
+def test_b16_walk_variants_bit_identical(tmp_path):
+    """The bf16 large-tile GEMMs compute every tile identically on the one-workgroup-per-tile grid
+    (K3M_B16_PERSIST=0), the persistent walk (default), the persistent walk with the ping-pong main loop on
+    every tile (K3M_B16_PP=7) and without the two-workgroups-per-CU GELU/dGELU kernel (K3M_B16_DUAL=0):
+    same MFMA order per accumulator, so bit-identical C, pre-activations, slabs and grouped outputs.  The
+    knobs are read at library load, so each setting runs in its own process."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "b16_walk_case.py"
+    script.write_text(_B16_WALK_SCRIPT)
+    res = {}
+    for name, knobs in (("tile", {"K3M_B16_PERSIST": "0", "K3M_B16_DUAL": "0"}),
+                        ("walk", {"K3M_B16_PERSIST": "1", "K3M_B16_PP": "0", "K3M_B16_DUAL": "0"}),
+                        ("pp", {"K3M_B16_PERSIST": "1", "K3M_B16_PP": "7", "K3M_B16_DUAL": "0"})):
+        path = str(tmp_path / ("out_%s.pt" % name))
+        env = dict(os.environ, **knobs)
+        subprocess.run([sys.executable, str(script), path, repo], check=True, env=env, timeout=240)
+        res[name] = torch.load(path, weights_only=True)
+    for name in ("walk", "pp"):
+        for k in res["tile"]:
+            assert torch.equal(res["tile"][k], res[name][k]), (name, k)
