@@ -262,7 +262,8 @@ struct PPHalf {
     }
   }
   // split + write the half tile into the three planes of one operand image (plane stride TILE * BK)
-  __device__ __forceinline__ void store(__bf16* __restrict__ lds, int t, int half) const {
+  __device__ __forceinline__ void store(__bf16* __restrict__ lds, int t, int half) const { store_from(r, lds, t, half); }
+  __device__ __forceinline__ void store_from(const floatx4 (&r)[NB], __bf16* __restrict__ lds, int t, int half) const {
     constexpr int PL = TILE * BK;
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -407,20 +408,141 @@ struct PPLoop {
   }
 };
 
-template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool PIPE, bool PP>
+// Ping-pong loop with LDS-DMA staging of the raw fp32 k-tiles (PP = 2, the 256x256 weight-gradient walk).
+// That walk streams both operands from HBM (K = 20,992 split 7-14 ways); PPLoop gives each register-staged
+// load two phases to land and its waves then wait (profiles/r5d/pmc_wgrad_ffn1_pingpong.json: MFMA busy 0.40, 57 % of
+// wave cycles parked in s_waitcnt).  Here every thread DMAs the float4s it will split (global_load_lds_dwordx4,
+// lane-linear 1 KiB per wave instruction) into one of two raw fp32 buffers behind the x6 stages (2 x 32 KiB;
+// 96 + 64 = 160 KiB of LDS), and reads them back itself: no barrier orders the raw buffers, only the issuing
+// wave's counted vmcnt.  M(t) splits k-tile t+1 from its raw buffer, then DMAs k-tile t+3 into the same
+// buffer: each DMA has two whole iterations to land, with no staging registers.  k-tile 0 still goes
+// through registers (loaded inside the previous tile's epilogue, as PPLoop).
+template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_>
+struct PPDLoop : PPLoop<TBM, TBN, WM, WN, BK, AK, BK_> {
+  using Base = PPLoop<TBM, TBN, WM, WN, BK, AK, BK_>;
+  using Base::ha;
+  using Base::hb;
+  using Base::lda;
+  using Base::ldb;
+  using Base::nt;
+  using Base::krem;
+  static constexpr int BUF = Base::BUF, PA = Base::PA, FM = Base::FM, FN = Base::FN, KS = Base::KS;
+  static constexpr int NBA = PPHalf<AK, TBM, BK>::NB, NBB = PPHalf<BK_, TBN, BK>::NB, ND = NBA + NBB;
+  static constexpr int RAW_FLOATS = 512 * 4 * ND;          // one raw k-tile: ND float4 per thread
+  static constexpr int RAW_OFF_BF16 = 2 * BUF;             // raw buffers start after the two x6 stages
+
+  // DMA this thread's float4s of the next k-tile into raw buffer rb and advance the pointers; lanes of a
+  // partial tile past krem read the tile's first k (valid) and are zeroed when split
+  // One LDS-DMA wave instruction as inline asm: issued through the builtin, the compiler's waitcnt pass
+  // (which cannot tell the raw buffers from the x6 stages) puts a vmcnt(0) before every later LDS read,
+  // i.e. waits for the DMAs still meant to be in flight.  Hidden from it, the DMAs are ordered only by
+  // the counted vmcnt waits of run() (the compiler's own vmcnt counts for register loads stay
+  // conservative: it sees fewer younger VMEM operations than there are).
+  __device__ __forceinline__ static void dma16(const float* g, const float* lds) {
+    const uint32_t m0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)lds;
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+  }
+  template <bool KC, int TILE>
+  __device__ __forceinline__ static void dma(PPHalf<KC, TILE, BK>& h, float* raw, int slot0, long long ld) {
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+    for (int b = 0; b < PPHalf<KC, TILE, BK>::NB; ++b) {
+      dma16(h.p[b], raw + ((slot0 + b) * 512 + w * 64) * 4);   // wave-uniform: lane l lands at + 4 l floats
+      h.p[b] += KC ? BK : BK * ld;
+    }
+  }
+  __device__ __forceinline__ void dma_tile(float* raw, int kk) {
+    // the partial tile: clamp the lanes past kk to the tile's first k (the pointers are restored after)
+    if (kk < BK) {
+#pragma unroll
+      for (int b = 0; b < NBA; ++b)
+        if (ha.kq[b] >= kk) ha.p[b] -= AK ? ha.kq[b] : (long long)ha.kq[b] * lda;
+#pragma unroll
+      for (int b = 0; b < NBB; ++b)
+        if (hb.kq[b] >= kk) hb.p[b] -= BK_ ? hb.kq[b] : (long long)hb.kq[b] * ldb;
+    }
+    dma<AK, TBM>(ha, raw, 0, lda);
+    dma<BK_, TBN>(hb, raw, NBA, ldb);
+  }
+  template <bool KC, int TILE>
+  __device__ __forceinline__ static void split_raw(const PPHalf<KC, TILE, BK>& h, const float* raw, int slot0,
+                                                  __bf16* stage, int kk) {
+    const int tid = threadIdx.x, t = tid & 255, half = tid >> 8;
+    floatx4 r[PPHalf<KC, TILE, BK>::NB];
+    const floatx4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int b = 0; b < PPHalf<KC, TILE, BK>::NB; ++b) {
+      const floatx4 v = *reinterpret_cast<const floatx4*>(raw + ((slot0 + b) * 512 + tid) * 4);
+      r[b] = h.kq[b] < kk ? v : z;
+    }
+    h.store_from(r, stage, t, half);
+  }
+
+  __device__ __forceinline__ void run(__bf16* smem, floatx16 (&acc)[FM][FN]) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const bool late = threadIdx.x >= 256;
+    float* raw0 = reinterpret_cast<float*>(smem + RAW_OFF_BF16);
+    auto rawbuf = [&](int t) { return raw0 + (t & 1) * RAW_FLOATS; };
+    if (nt > 0) this->stage_half(smem);                  // k-tile 0 from registers
+    if (nt > 1) dma_tile(rawbuf(1), this->tile_k(1));
+    if (nt > 2) dma_tile(rawbuf(2), this->tile_k(2));
+    pp_barrier();
+    if (late) pp_barrier();
+#pragma nounroll
+    for (int kt = 0; kt < nt; ++kt) {
+      const int cur = kt & 1;
+      bf16x8 a[KS][3][FM], b[KS][3][FN];
+      this->frags(smem + cur * BUF, a, b);
+      if (kt + 1 < nt) {
+        __builtin_amdgcn_sched_barrier(0);
+        // gfx9 s_waitcnt simm16: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14
+        static_assert(ND < 16, "vmcnt immediate");
+        if (kt + 2 < nt) __builtin_amdgcn_s_waitcnt(0x0F70 | ND);   // vmcnt(ND): k-tile t+2's DMAs may fly on
+        else __builtin_amdgcn_s_waitcnt(0x0F70);                    // vmcnt(0)
+        __builtin_amdgcn_sched_barrier(0);
+        const int kk = this->tile_k(kt + 1);
+        __bf16* st = smem + (cur ^ 1) * BUF;
+        split_raw<AK, TBM>(ha, rawbuf(kt + 1), 0, st, kk);
+        split_raw<BK_, TBN>(hb, rawbuf(kt + 1), NBA, st + 3 * PA, kk);
+        if (kt + 3 < nt) {
+          __builtin_amdgcn_s_waitcnt(0xC07F);   // this wave's reads of the raw buffer are back
+          __builtin_amdgcn_sched_barrier(0);
+          dma_tile(rawbuf(kt + 3), this->tile_k(kt + 3));
+        }
+      }
+      pp_barrier();
+      Base::mfma(a, b, acc);
+      pp_barrier();
+    }
+    if (!late) pp_barrier();
+  }
+};
+
+template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool PIPE, int PP>
 struct LoopSel {
   using T = Loop<TBM, TBN, WM, WN, BK, AK, BK_, PIPE>;
 };
 template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool PIPE>
-struct LoopSel<TBM, TBN, WM, WN, BK, AK, BK_, PIPE, true> {
+struct LoopSel<TBM, TBN, WM, WN, BK, AK, BK_, PIPE, 1> {
   using T = PPLoop<TBM, TBN, WM, WN, BK, AK, BK_>;
 };
+template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool PIPE>
+struct LoopSel<TBM, TBN, WM, WN, BK, AK, BK_, PIPE, 2> {
+  using T = PPDLoop<TBM, TBN, WM, WN, BK, AK, BK_>;
+};
 
-template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, int EPI, bool PIPE, bool PP = false>
+// PP: 0 the compiler-scheduled loop (Loop), 1 the ping-pong loop (PPLoop), 2 with LDS-DMA staging (PPDLoop)
+template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, int EPI, bool PIPE, int PP = 0>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_x6_persist_kernel(GemmGroup grp) {
   constexpr int LDS_BF16 = 2 * 3 * (TBM + TBN) * BK;
   constexpr int EPI_F32 = WM * WN * 32 * (TBN / WN + 8);
-  constexpr int WORDS = (LDS_BF16 / 2 > EPI_F32 ? LDS_BF16 / 2 : EPI_F32);
+  constexpr int RAW = PP == 2 ? 2 * PPDLoop<TBM, TBN, WM, WN, BK, AK, BK_>::RAW_FLOATS : 0;
+  constexpr int WORDS = (LDS_BF16 / 2 + RAW > EPI_F32 ? LDS_BF16 / 2 + RAW : EPI_F32);
   __shared__ __attribute__((aligned(16))) float smem[WORDS];
   const int total = grp.start[grp.count];
   int u = blockIdx.x;
@@ -449,7 +571,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_x6_persist_kernel(GemmGr
   }
 }
 
-template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool PIPE, bool PP = false>
+template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_, bool PIPE, int PP = 0>
 int launch(const GemmGroup& grp, int epi, int nblk, hipStream_t st) {
   const dim3 grid(nblk);
   switch (epi) {
@@ -493,21 +615,21 @@ int k3m_x6_persistent_launch(const k3m_x6::GemmGroup& grp, bool t256, bool ak, b
   const int cls = ak && bk ? 1 : ak ? 2 : !bk ? 4 : 8;
   const bool pp = (kPP & cls) != 0 && (t256 ? (cls != 4 || (kPP & 32) != 0) : (kPP & 16) != 0);
   if (t256) {
-    if (ak && bk) return pp ? launch<256, 256, 4, 2, 16, true, true, true, true>(grp, epi, nblk, st)
+    if (ak && bk) return pp ? launch<256, 256, 4, 2, 16, true, true, true, 1>(grp, epi, nblk, st)
                             : launch<256, 256, 4, 2, 16, true, true, true>(grp, epi, nblk, st);
-    if (ak) return pp ? launch<256, 256, 2, 4, 16, true, false, true, true>(grp, epi, nblk, st)
+    if (ak) return pp ? launch<256, 256, 2, 4, 16, true, false, true, 1>(grp, epi, nblk, st)
                       : launch<256, 256, 2, 4, 16, true, false, true>(grp, epi, nblk, st);
-    if (!bk) return pp ? launch<256, 256, 2, 4, 16, false, false, false, true>(grp, epi, nblk, st)
+    if (!bk) return pp ? launch<256, 256, 2, 4, 16, false, false, false, 2>(grp, epi, nblk, st)
                        : launch<256, 256, 2, 4, 16, false, false, false>(grp, epi, nblk, st);
     return K3M_EINVAL;
   }
-  if (ak && bk) return pp ? launch<256, 128, 4, 2, 32, true, true, true, true>(grp, epi, nblk, st)
+  if (ak && bk) return pp ? launch<256, 128, 4, 2, 32, true, true, true, 1>(grp, epi, nblk, st)
                           : launch<256, 128, 4, 2, 32, true, true, true>(grp, epi, nblk, st);
-  if (ak) return pp ? launch<256, 128, 4, 2, 32, true, false, true, true>(grp, epi, nblk, st)
+  if (ak) return pp ? launch<256, 128, 4, 2, 32, true, false, true, 1>(grp, epi, nblk, st)
                     : launch<256, 128, 4, 2, 32, true, false, true>(grp, epi, nblk, st);
-  if (bk) return pp ? launch<256, 128, 4, 2, 32, false, true, true, true>(grp, epi, nblk, st)
+  if (bk) return pp ? launch<256, 128, 4, 2, 32, false, true, true, 1>(grp, epi, nblk, st)
                     : launch<256, 128, 4, 2, 32, false, true, true>(grp, epi, nblk, st);
-  return pp ? launch<256, 128, 4, 2, 32, false, false, false, true>(grp, epi, nblk, st)
+  return pp ? launch<256, 128, 4, 2, 32, false, false, false, 1>(grp, epi, nblk, st)
             : launch<256, 128, 4, 2, 32, false, false, false>(grp, epi, nblk, st);
 }
 

@@ -212,7 +212,8 @@ torch.save({k: v.cpu() for k, v in out.items()}, sys.argv[1])
 def test_persistent_walk_bit_identical(tmp_path):
     """The persistent x6 walk (gemm_x6p.hip, K3M_X6_PERSIST=1, default) computes every tile exactly as the
     one-workgroup-per-tile kernels (K3M_X6_PERSIST=0): bit-identical C, aux, split-K sums and grouped
-    outputs, and so do the persistent walks with the ping-pong main loop (K3M_X6_PP=31, every layout and tile)
+    outputs, and so do the persistent walks with the ping-pong main loops (K3M_X6_PP=63: every layout and tile, the
+    256x256 weight-gradient walk on the LDS-DMA-staged form)
     and with it off (K3M_X6_PP=0).  The knobs are read at library load, so each setting runs in its own
     process."""
     import os
@@ -223,7 +224,7 @@ def test_persistent_walk_bit_identical(tmp_path):
     script.write_text(_PERSIST_SCRIPT)
     res = {}
     for name, knobs in (("tile", {"K3M_X6_PERSIST": "0"}), ("walk", {"K3M_X6_PERSIST": "1", "K3M_X6_PP": "0"}),
-                        ("pp", {"K3M_X6_PERSIST": "1", "K3M_X6_PP": "31"})):
+                        ("pp", {"K3M_X6_PERSIST": "1", "K3M_X6_PP": "63"})):
         path = str(tmp_path / ("out_%s.pt" % name))
         env = dict(os.environ, **knobs)
         subprocess.run([sys.executable, str(script), path, repo], check=True, env=env, timeout=240)
