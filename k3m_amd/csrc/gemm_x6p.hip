@@ -594,7 +594,8 @@ int launch(const GemmGroup& grp, int epi, int nblk, hipStream_t st) {
 
 // K3M_X6_PP: ping-pong main loop (PPLoop) per operand-layout class, bitmask: 1 forward (both K-contiguous),
 // 2 input gradient (B MN-contiguous), 4 weight gradient (both MN-contiguous), 8 A MN-contiguous / B
-// K-contiguous; 16 = the 256x128 tiles too; 32 = the 256x256 weight-gradient walk too.  Default 31: same box,
+// K-contiguous; 16 = the 256x128 tiles too; 32 = the 256x256 weight-gradient walk too (on the LDS-DMA-staged
+// PPDLoop); 64 = the 256x256 forward / input-gradient walks on PPDLoop as well (A/B).  Default 31: same box,
 // interleaved (profiles/r5d/ab_x6_pp_gemm_shapes.txt) the K-contiguous 256x256 forwards / input gradients 4-7 % faster
 // (FFN2 0.460 -> 0.430 ms), the 256x128 and image / co-attention shapes 5-15 %, the dGELU input gradient
 // equal, but the 256x256 weight-gradient walk (both operands streamed from HBM, K = 20,992) 22-27 % SLOWER:
@@ -615,10 +616,12 @@ int k3m_x6_persistent_launch(const k3m_x6::GemmGroup& grp, bool t256, bool ak, b
   const int cls = ak && bk ? 1 : ak ? 2 : !bk ? 4 : 8;
   const bool pp = (kPP & cls) != 0 && (t256 ? (cls != 4 || (kPP & 32) != 0) : (kPP & 16) != 0);
   if (t256) {
-    if (ak && bk) return pp ? launch<256, 256, 4, 2, 16, true, true, true, 1>(grp, epi, nblk, st)
-                            : launch<256, 256, 4, 2, 16, true, true, true>(grp, epi, nblk, st);
-    if (ak) return pp ? launch<256, 256, 2, 4, 16, true, false, true, 1>(grp, epi, nblk, st)
-                      : launch<256, 256, 2, 4, 16, true, false, true>(grp, epi, nblk, st);
+    if (ak && bk) return !pp ? launch<256, 256, 4, 2, 16, true, true, true>(grp, epi, nblk, st)
+                      : (kPP & 64) ? launch<256, 256, 4, 2, 16, true, true, true, 2>(grp, epi, nblk, st)
+                                   : launch<256, 256, 4, 2, 16, true, true, true, 1>(grp, epi, nblk, st);
+    if (ak) return !pp ? launch<256, 256, 2, 4, 16, true, false, true>(grp, epi, nblk, st)
+                : (kPP & 64) ? launch<256, 256, 2, 4, 16, true, false, true, 2>(grp, epi, nblk, st)
+                             : launch<256, 256, 2, 4, 16, true, false, true, 1>(grp, epi, nblk, st);
     if (!bk) return pp ? launch<256, 256, 2, 4, 16, false, false, false, 2>(grp, epi, nblk, st)
                        : launch<256, 256, 2, 4, 16, false, false, false>(grp, epi, nblk, st);
     return K3M_EINVAL;

@@ -213,7 +213,7 @@ def test_persistent_walk_bit_identical(tmp_path):
     """The persistent x6 walk (gemm_x6p.hip, K3M_X6_PERSIST=1, default) computes every tile exactly as the
     one-workgroup-per-tile kernels (K3M_X6_PERSIST=0): bit-identical C, aux, split-K sums and grouped
     outputs, and so do the persistent walks with the ping-pong main loops (K3M_X6_PP=63: every layout and tile, the
-    256x256 weight-gradient walk on the LDS-DMA-staged form)
+    256x256 weight-gradient walk on the LDS-DMA-staged form; K3M_X6_PP=127: every 256x256 walk on it)
     and with it off (K3M_X6_PP=0).  The knobs are read at library load, so each setting runs in its own
     process."""
     import os
@@ -224,12 +224,13 @@ def test_persistent_walk_bit_identical(tmp_path):
     script.write_text(_PERSIST_SCRIPT)
     res = {}
     for name, knobs in (("tile", {"K3M_X6_PERSIST": "0"}), ("walk", {"K3M_X6_PERSIST": "1", "K3M_X6_PP": "0"}),
-                        ("pp", {"K3M_X6_PERSIST": "1", "K3M_X6_PP": "63"})):
+                        ("pp", {"K3M_X6_PERSIST": "1", "K3M_X6_PP": "63"}),
+                        ("ppd", {"K3M_X6_PERSIST": "1", "K3M_X6_PP": "127"})):
         path = str(tmp_path / ("out_%s.pt" % name))
         env = dict(os.environ, **knobs)
         subprocess.run([sys.executable, str(script), path, repo], check=True, env=env, timeout=240)
         res[name] = torch.load(path, weights_only=True)
-    for name in ("walk", "pp"):
+    for name in ("walk", "pp", "ppd"):
         for k in res["tile"]:
             assert torch.equal(res["tile"][k], res[name][k]), (name, k)
 
