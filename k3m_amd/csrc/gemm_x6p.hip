@@ -464,18 +464,26 @@ struct PPDLoop : PPLoop<TBM, TBN, WM, WN, BK, AK, BK_> {
     dma<AK, TBM>(ha, raw, 0, lda);
     dma<BK_, TBN>(hb, raw, NBA, ldb);
   }
-  template <bool KC, int TILE>
-  __device__ __forceinline__ static void split_raw(const PPHalf<KC, TILE, BK>& h, const float* raw, int slot0,
-                                                  __bf16* stage, int kk) {
+  // read back this thread's float4s of one raw k-tile, one operand's reads issued together (a serial
+  // read -> split -> read chain costs one LDS round trip per float4; all four at once spill), zero a partial
+  // tile's lanes past kk, split and write both operands' halves into the x6 stage
+  __device__ __forceinline__ void split_raw(const float* raw, __bf16* stage, int kk) const {
     const int tid = threadIdx.x, t = tid & 255, half = tid >> 8;
-    floatx4 r[PPHalf<KC, TILE, BK>::NB];
     const floatx4 z = {0.f, 0.f, 0.f, 0.f};
+    floatx4 ra[NBA];
 #pragma unroll
-    for (int b = 0; b < PPHalf<KC, TILE, BK>::NB; ++b) {
-      const floatx4 v = *reinterpret_cast<const floatx4*>(raw + ((slot0 + b) * 512 + tid) * 4);
-      r[b] = h.kq[b] < kk ? v : z;
-    }
-    h.store_from(r, stage, t, half);
+    for (int b = 0; b < NBA; ++b) ra[b] = *reinterpret_cast<const floatx4*>(raw + (b * 512 + tid) * 4);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int b = 0; b < NBA; ++b) ra[b] = ha.kq[b] < kk ? ra[b] : z;
+    ha.store_from(ra, stage, t, half);
+    floatx4 rb[NBB];
+#pragma unroll
+    for (int b = 0; b < NBB; ++b) rb[b] = *reinterpret_cast<const floatx4*>(raw + ((NBA + b) * 512 + tid) * 4);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int b = 0; b < NBB; ++b) rb[b] = hb.kq[b] < kk ? rb[b] : z;
+    hb.store_from(rb, stage + 3 * PA, t, half);
   }
 
   __device__ __forceinline__ void run(__bf16* smem, floatx16 (&acc)[FM][FN]) {
@@ -507,8 +515,7 @@ struct PPDLoop : PPLoop<TBM, TBN, WM, WN, BK, AK, BK_> {
         __builtin_amdgcn_sched_barrier(0);
         const int kk = this->tile_k(kt + 1);
         __bf16* st = smem + (cur ^ 1) * BUF;
-        split_raw<AK, TBM>(ha, rawbuf(kt + 1), 0, st, kk);
-        split_raw<BK_, TBN>(hb, rawbuf(kt + 1), NBA, st + 3 * PA, kk);
+        split_raw(rawbuf(kt + 1), st, kk);
         if (kt + 3 < nt) {
           __builtin_amdgcn_s_waitcnt(0xC07F);   // this wave's reads of the raw buffer are back
           __builtin_amdgcn_sched_barrier(0);
