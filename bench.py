@@ -243,7 +243,7 @@ def head_kernel(bf):
         return "k3m_x6::gemm_x6_kernel<256, 256"
     # the FFN1 forward (both operands K-contiguous, bias+GELU epilogue = 2); last argument: the ping-pong main
     # loop (K3M_X6_PP bit 0, on by default)
-    pp = (int(os.environ.get("K3M_X6_PP", "31")) & 1) != 0
+    pp = (int(os.environ.get("K3M_X6_PP", "63")) & 1) != 0
     return "k3m_x6::gemm_x6_persist_kernel<256, 256, 4, 2, 16, true, true, 2, true, %s>" % ("true" if pp else "false")
 
 

@@ -599,15 +599,16 @@ int launch(const GemmGroup& grp, int epi, int nblk, hipStream_t st) {
   return 0;
 }
 
-// K3M_X6_PP: ping-pong main loop (PPLoop) per operand-layout class, bitmask: 1 forward (both K-contiguous),
-// 2 input gradient (B MN-contiguous), 4 weight gradient (both MN-contiguous), 8 A MN-contiguous / B
-// K-contiguous; 16 = the 256x128 tiles too; 32 = the 256x256 weight-gradient walk too (on the LDS-DMA-staged
-// PPDLoop); 64 = the 256x256 forward / input-gradient walks on PPDLoop as well (A/B).  Default 31: same box,
-// interleaved (profiles/r5d/ab_x6_pp_gemm_shapes.txt) the K-contiguous 256x256 forwards / input gradients 4-7 % faster
-// (FFN2 0.460 -> 0.430 ms), the 256x128 and image / co-attention shapes 5-15 %, the dGELU input gradient
-// equal, but the 256x256 weight-gradient walk (both operands streamed from HBM, K = 20,992) 22-27 % SLOWER:
-// its loads get two phases (one k-tile of the faster loop) to land and do not.
-const int kPP = k3m_env_int("K3M_X6_PP", 31);
+// K3M_X6_PP: ping-pong main loops per operand-layout class, bitmask: 1 forward (both K-contiguous), 2 input
+// gradient (B MN-contiguous), 4 weight gradient (both MN-contiguous), 8 A MN-contiguous / B K-contiguous;
+// 16 = the 256x128 tiles too; 32 = the 256x256 weight-gradient walk too, on the LDS-DMA-staged PPDLoop;
+// 64 = the 256x256 forward / input-gradient walks on PPDLoop as well (A/B only).  Default 63, each part
+// measured same box, interleaved (profiles/r5d/README.txt): PPLoop on the K-contiguous 256x256 forwards / input
+// gradients 4-7 % faster than the compiler-scheduled walk, on the 256x128 and image / co-attention shapes
+// 5-15 %; the 256x256 weight gradients 22-27 % SLOWER on PPLoop (HBM-streamed operands, loads with two phases to
+// land) and 1-3 % faster on PPDLoop; PPDLoop on the forwards 3-4 % slower than PPLoop.  Config 2: walk 527 ->
+// PPLoop 541 -> + PPDLoop weight gradients 542 samples/s.
+const int kPP = k3m_env_int("K3M_X6_PP", 63);
 
 }  // namespace
 }  // namespace k3m_x6
