@@ -241,10 +241,10 @@ def head_kernel(bf):
             else "k3m_b16::gemm_kernel<256, 256"
     if os.environ.get("K3M_X6_PERSIST", "1") == "0":
         return "k3m_x6::gemm_x6_kernel<256, 256"
-    # the FFN1 forward (both operands K-contiguous, bias+GELU epilogue = 2); last argument: the ping-pong main
-    # loop (K3M_X6_PP bit 0, on by default)
+    # the FFN1 forward (both operands K-contiguous, bias+GELU epilogue = 2); last argument: the main loop
+    # (0 compiler-scheduled, 1 ping-pong: K3M_X6_PP bit 0, on by default)
     pp = (int(os.environ.get("K3M_X6_PP", "63")) & 1) != 0
-    return "k3m_x6::gemm_x6_persist_kernel<256, 256, 4, 2, 16, true, true, 2, true, %s>" % ("true" if pp else "false")
+    return "k3m_x6::gemm_x6_persist_kernel<256, 256, 4, 2, 16, true, true, 2, true, %d>" % (1 if pp else 0)
 
 
 def pmc_traffic(key, kernel):
