@@ -293,6 +293,20 @@ __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// lab-only issue priority variants of the ping-pong phases (scripts/lab/lab_build.sh -D...): the M-phase wave
+// ahead of its MFMA partner for VALU / LDS issue (K3M_LAB_PP_PRIO), or waves 4-7 statically ahead
+// (K3M_LAB_PP_PRIO_LATE, MI355X_MICROARCH.md "Two waves per SIMD" item 4)
+__device__ __forceinline__ void pp_prio_m() {
+#ifdef K3M_LAB_PP_PRIO
+  __builtin_amdgcn_s_setprio(1);
+#endif
+}
+__device__ __forceinline__ void pp_prio_c() {
+#ifdef K3M_LAB_PP_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
+}
+
 template <int TBM, int TBN, int WM, int WN, int BK, bool AK, bool BK_>
 struct PPLoop {
   static_assert(WM * WN == 8, "ping-pong pairs waves w and w + 4 of an 8-wave workgroup");
@@ -388,9 +402,13 @@ struct PPLoop {
     }
     pp_barrier();
     if (late) pp_barrier();
+#ifdef K3M_LAB_PP_PRIO_LATE
+    if (late) __builtin_amdgcn_s_setprio(1);
+#endif
     for (int kt = 0; kt < nt; ++kt) {
       const int cur = kt & 1;
       bf16x8 a[KS][3][FM], b[KS][3][FN];
+      pp_prio_m();
       frags(smem + cur * BUF, a, b);
       if (kt + 1 < nt) {
         stage_half(smem + (cur ^ 1) * BUF);
@@ -401,9 +419,13 @@ struct PPLoop {
         }
       }
       pp_barrier();
+      pp_prio_c();
       mfma(a, b, acc);
       pp_barrier();
     }
+#if defined(K3M_LAB_PP_PRIO) || defined(K3M_LAB_PP_PRIO_LATE)
+    __builtin_amdgcn_s_setprio(0);
+#endif
     if (!late) pp_barrier();
   }
 };
