@@ -36,7 +36,11 @@ __device__ __forceinline__ Unit decode(const GemmGroup& grp, int u) {
   const int local = id - grp.start[r.p];
   r.slice = local / tiles;
   const int t = local - r.slice * tiles;
+#ifdef K3M_LAB_GROUP   // lab: row-tiles per N walk (scripts/lab/lab_build.sh -DK3M_LAB_GROUP=4)
+  constexpr int GROUP = K3M_LAB_GROUP;
+#else
   constexpr int GROUP = 8;
+#endif
   const int group_sz = GROUP * tn, first_m = (t / group_sz) * GROUP, gm_sz = min(tm - first_m, GROUP);
   r.m0 = (first_m + (t % group_sz) % gm_sz) * TBM;
   r.n0 = ((t % group_sz) / gm_sz) * TBN;
