@@ -465,8 +465,11 @@ struct PPDLoop : PPLoop<TBM, TBN, WM, WN, BK, AK, BK_> {
   // the counted vmcnt waits of run() (the compiler's own vmcnt counts for register loads stay
   // conservative: it sees fewer younger VMEM operations than there are).
   __device__ __forceinline__ static void dma16(const float* g, const float* lds) {
+    // M0 = the wave-uniform LDS destination, written by the compiler through the "{m0}" operand (a clobbered
+    // M0 would be a reserved-register clobber); s_nop 0: the M0 write -> LDS-DMA hazard
     const uint32_t m0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)lds;
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(__builtin_amdgcn_readfirstlane(m0))
+                 : "memory");
   }
   template <bool KC, int TILE>
   __device__ __forceinline__ static void dma(PPHalf<KC, TILE, BK>& h, float* raw, int slot0, long long ld) {
