@@ -16,9 +16,13 @@ itself, before touching the GPU, and exits with its status.  Each rank runs its 
 max over ranks is taken.
 
 Rank 0 prints ONE JSON line with the driver's contract plus
-  roofline        — the dominant kernel (the text-layer FFN1 GEMM, 2BT+2BP rows x 3072 x 768),
+  roofline        — the dominant kernel by time (the 256x256 weight-gradient walk, ~21 % of the fp32 step) on its
+                    largest launch shape, the text-layer FFN1 weight gradient (3072 x 768 x 2BT+2BP rows),
                     timed with HIP events on its stream over the timed steps, against the peak of the
                     arithmetic it runs on (fp32: bf16x6 split = bf16 dense peak / 6; bf16: bf16 peak);
+                    ``class``: every text-layer weight gradient on that kernel;
+  roofline_ffn1   — the text-layer FFN1 forward GEMM (2BT+2BP rows x 3072 x 768, bias+GELU), as rounds 1-5;
+  parity          — the engine's five losses against the CPU oracle's on the CPU baseline's bs=64 batch;
   coattn          — the co-attention blocks (18 layers: both directions' attention, projections,
                     FFNs, LayerNorms; forward + backward) timed with HIP events: their algorithmic
                     FLOPs / time against the same peak (north-star target >= 0.40);
@@ -111,11 +115,13 @@ def launch_ranks(args):
 
 
 class GemmProbe(object):
-    """Times every launch of one GEMM shape with HIP events on the launching stream."""
+    """Times every launch of one GEMM shape (or of a set of shapes) with HIP events on the launching stream."""
 
-    def __init__(self, m, n, k):
+    def __init__(self, m, n, k, more=()):
         self.key = (m, n, k)
+        self.keys = {self.key} | set(more)
         self.events = []
+        self.shapes = []
         self.active = False
 
     def install(self):
@@ -125,21 +131,35 @@ class GemmProbe(object):
         probe = self
 
         def wrapped(a, a_trans, b, b_trans, c, m, n, k, *args, **kw):
-            if probe.active and (m, n, k) == probe.key and ops._grouper is None:   # a deferred GEMM is not timed here
+            if probe.active and (m, n, k) in probe.keys and ops._grouper is None:   # a deferred GEMM is not timed here
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
                 r = orig(a, a_trans, b, b_trans, c, m, n, k, *args, **kw)
                 e.record()
                 probe.events.append((s, e))
+                probe.shapes.append((m, n, k))
                 return r
             return orig(a, a_trans, b, b_trans, c, m, n, k, *args, **kw)
 
+        prev = ops.gemm
         ops.gemm = wrapped
+        return prev
 
-    def mean_ms(self):
-        if not self.events:
+    def launches(self, key=None):
+        return [se for se, sh in zip(self.events, self.shapes) if key is None or sh == key]
+
+    def mean_ms(self, key=None):
+        ev = self.launches(key if key is not None else self.key)
+        if not ev:
             return None
-        return sum(s.elapsed_time(e) for s, e in self.events) / len(self.events)
+        return sum(s.elapsed_time(e) for s, e in ev) / len(ev)
+
+    def aggregate(self):
+        """(launches, total ms, total FLOPs) over every probed launch of every probed shape."""
+        if not self.events:
+            return 0, 0.0, 0.0
+        return (len(self.events), sum(s.elapsed_time(e) for s, e in self.events),
+                sum(2.0 * m * n * k for m, n, k in self.shapes))
 
 
 class CoattnProbe(object):
@@ -247,6 +267,19 @@ def head_kernel(bf):
     return "k3m_x6::gemm_x6_persist_kernel<256, 256, 4, 2, 16, true, true, 2, true, %d>" % (1 if pp else 0)
 
 
+def head_wgrad_kernel(bf):
+    """Full-name fragment of the kernel the text-layer weight gradients (tn, k = 20,992 split over k) run on at HEAD:
+    the 256x256 walk with both operands MN-contiguous and no epilogue; fp32: the last argument is the main loop
+    (2 = PPDLoop, LDS-DMA staged raw tiles, K3M_X6_PP bits 1|2 on by default)."""
+    if bf:
+        return "k3m_b16::gemm_persist_kernel<256, 256, 2, 4, false, false, 0, float, 32, false>"
+    if os.environ.get("K3M_X6_PERSIST", "1") == "0":
+        return "k3m_x6::gemm_x6_kernel<256, 256"
+    pp = int(os.environ.get("K3M_X6_PP", "63"))
+    loop = 2 if (pp & 4 and pp & 32) else (1 if pp & 4 else 0)   # gemm_x6p.hip kPP: 4 weight gradients, 32 on PPDLoop
+    return "k3m_x6::gemm_x6_persist_kernel<256, 256, 2, 4, 16, false, false, 0, false, %d>" % loop
+
+
 def pmc_traffic(key, kernel):
     """HBM-side bytes per launch of the probed GEMM from the newest committed rocprofv3 PMC record of THIS
     kernel and shape (profiles/r*_pmc_*.json from scripts/pmc_gemm.sh + scripts/pmc_table.py: FETCH_SIZE x2
@@ -294,42 +327,73 @@ def cpu_share():
                                                                       os.cpu_count() or 0)
 
 
-def cpu_baseline(cfg, shape, bsz, steps):
+PARITY_LOSSES = ("masked_lm_loss", "masked_img_loss", "masked_lm_loss_pv", "loss_lpm", "next_sentence_loss", "loss")
+
+
+def parity_inputs(cfg, shape, b, device):
+    """The CPU baseline's batch, gumbel noise and LPM negative tables (seeded, identical on every device)."""
+    import torch
+    from k3m_amd.synthetic import synthetic_batch, synthetic_noise
+    T, Pl, nbox = shape["T"], shape["P"], shape["nbox"]
+    batch = synthetic_batch(cfg, b, "cpu", seed=99, T=T, P=Pl, n_boxes=nbox, n_triples=shape["n_triples"],
+                            npv=shape["npv"])
+    noise = synthetic_noise(cfg, b, seed=1, T=T, P=Pl, R=nbox + 1)
+    NPV = batch["index_p"].shape[1]
+    nt = shape["n_triples"]
+    ent = torch.full((b, NPV, 2), -1, dtype=torch.int64)
+    val = torch.full((b, NPV, 2), -1, dtype=torch.int64)
+    for i in range(b):
+        for j in range(nt):
+            ent[i, j, 0] = (i + 1) % b if b > 1 else -1
+            ent[i, j, 1] = (i + 2) % b if b > 2 else -1
+            val[i, j, 0] = (j + 1) % nt
+            val[i, j, 1] = (j + 2) % nt
+    if device != "cpu":
+        batch = {k: v.to(device) for k, v in batch.items()}
+        noise = {k: v.to(device) for k, v in noise.items()}
+    return batch, noise, ent, val
+
+
+def gpu_parity_losses(tr, cfg, shape, bsz):
+    """The HIP engine's eval-mode losses on the CPU baseline's first timed batch, from the oracle's starting weights
+    (init_values(cfg, 0), the reference initialisation): the GPU half of the full-size parity field (VERDICT r5
+    item 3; north_star "loss parity <= 1e-3 vs CPU reference").  Runs after the timed region on the bench's own
+    engine (its trained weights are overwritten: the bench is done with them)."""
+    import torch
+    from k3m_amd.weights import init_values
+    eng = tr.engine
+    eng.fp.load(init_values(cfg, 0))
+    batch, noise, ent, val = parity_inputs(cfg, shape, bsz, eng.fp.device)
+    with torch.no_grad():
+        out, _ = eng.forward(batch, train=False, noise=noise, ent_neg=ent, val_neg=val)
+    torch.cuda.synchronize()
+    return {k: float(out[k]) for k in PARITY_LOSSES}
+
+
+def cpu_baseline(cfg, shape, bsz, steps, gpu_losses=None, bar=1e-3):
     """Oracle (torch CPU fp32) fwd+bwd+AdamW on a bounded sample of the same workload; baseline only.
     Threads: this process's CPU share on the GPU box (os.sched_getaffinity), not the machine's nproc
     (reported beside it).  One bs=8 warm-up step, a bs=8 sample (2 timed steps), then
-    ``steps`` timed steps at ``bsz`` (the GPU workload's batch)."""
+    ``steps`` timed steps at ``bsz`` (the GPU workload's batch).  The bs=``bsz`` steps start from the initial weights
+    (restored after the bs=8 steps), so the first one's forward is also the oracle half of the parity field: its five
+    losses against ``gpu_losses`` (the engine on the same batch, weights, noise and negatives)."""
     import torch
     from oracle import k3m_oracle as O
     from k3m_amd.weights import init_values
-    from k3m_amd.synthetic import synthetic_batch, synthetic_noise
     ncores, share = cpu_share()
     torch.set_num_threads(ncores)
     P = {k: torch.from_numpy(v).requires_grad_(True) for k, v in init_values(cfg, 0).items()}
-    T, Pl, nbox = shape["T"], shape["P"], shape["nbox"]
+    P0 = {k: v.detach().clone() for k, v in P.items()}
     state = {k: (torch.zeros_like(v), torch.zeros_like(v)) for k, v in P.items()}
 
-    def make(b):
-        batch = synthetic_batch(cfg, b, "cpu", seed=99, T=T, P=Pl, n_boxes=nbox, n_triples=shape["n_triples"],
-                                npv=shape["npv"])
-        noise = synthetic_noise(cfg, b, seed=1, T=T, P=Pl, R=nbox + 1)
-        NPV = batch["index_p"].shape[1]
-        nt = shape["n_triples"]
-        ent = torch.full((b, NPV, 2), -1, dtype=torch.int64)
-        val = torch.full((b, NPV, 2), -1, dtype=torch.int64)
-        for i in range(b):
-            for j in range(nt):
-                ent[i, j, 0] = (i + 1) % b if b > 1 else -1
-                ent[i, j, 1] = (i + 2) % b if b > 2 else -1
-                val[i, j, 0] = (j + 1) % nt
-                val[i, j, 1] = (j + 2) % nt
-        return batch, noise, ent, val
-
     tstep = [0]
+    first = {}
 
     def step(inp):
         tstep[0] += 1
         out = O.forward(P, cfg, *inp)
+        if not first and inp[0]["input_ids"].shape[0] == bsz and tstep[0] == 1:
+            first.update({k: float(out[k]) for k in PARITY_LOSSES})
         out["loss"].backward()
         with torch.no_grad():
             for k, p in P.items():
@@ -339,26 +403,44 @@ def cpu_baseline(cfg, shape, bsz, steps):
                 O.adamw_step(p.data, p.grad, m, v, tstep[0], 1e-4, 0.0 if ("bias" in k or "LayerNorm" in k) else 0.01)
                 p.grad = None
 
-    small = make(8)
+    small = parity_inputs(cfg, shape, 8, "cpu")
     step(small)
     t0 = time.perf_counter()
     for _ in range(2):
         step(small)
     dt8 = time.perf_counter() - t0
-    big = make(bsz) if bsz != 8 else small
+    # back to the initial weights and a fresh optimizer for the timed bs=bsz steps (same work per step)
+    with torch.no_grad():
+        for k, p in P.items():
+            p.copy_(P0[k])
+            state[k][0].zero_()
+            state[k][1].zero_()
+    tstep[0] = 0
+    big = parity_inputs(cfg, shape, bsz, "cpu") if bsz != 8 else small
     t0 = time.perf_counter()
     for _ in range(steps):
         step(big)
     dt = time.perf_counter() - t0
-    return {"value": round(bsz * steps / dt, 4), "unit": "samples/s", "cores": ncores, "kind": "port",
-            "nproc": os.cpu_count(), "cpu_share": share, "cpu_model": cpu_model(),
-            "bs8_samples_s": round(8 * 2 / dt8, 4),
-            "sample": "oracle/k3m_oracle.py fwd+bwd+AdamW, fp32, bs=%d, %d timed step(s) (%.1f s) after a bs=8 warm-up; "
-                      "bs=8: 2 timed steps %.1f s (same shapes as the GPU workload; torch CPU, %d threads = this "
-                      "process's CPU share; the machine has %d).  Bounded sample: the bench contract asks for ~10-30 s "
-                      "of CPU work so the default run ends in minutes, so bs=64 runs %d step(s), not SURVEY §8(d)'s 3 "
-                      "after 1 warm-up (--cpu-steps 3 runs those)" % (bsz, steps, dt, dt8, ncores, os.cpu_count() or 0,
-                                                                       steps)}
+    res = {"value": round(bsz * steps / dt, 4), "unit": "samples/s", "cores": ncores, "kind": "port",
+           "nproc": os.cpu_count(), "cpu_share": share, "cpu_model": cpu_model(),
+           "bs8_samples_s": round(8 * 2 / dt8, 4),
+           "sample": "oracle/k3m_oracle.py fwd+bwd+AdamW, fp32, bs=%d, %d timed step(s) (%.1f s) after a bs=8 warm-up; "
+                     "bs=8: 2 timed steps %.1f s (same shapes as the GPU workload; torch CPU, %d threads = this "
+                     "process's CPU share; the machine has %d).  Bounded sample: the bench contract asks for ~10-30 s "
+                     "of CPU work so the default run ends in minutes, so bs=64 runs %d step(s), not SURVEY §8(d)'s 3 "
+                     "after 1 warm-up (--cpu-steps 3 runs those)" % (bsz, steps, dt, dt8, ncores, os.cpu_count() or 0,
+                                                                      steps)}
+    parity = None
+    if gpu_losses is not None and first:
+        rel = {k: abs(gpu_losses[k] - first[k]) / max(abs(first[k]), 1e-3) for k in PARITY_LOSSES}
+        parity = {"loss_gpu": {k: round(v, 7) for k, v in gpu_losses.items()},
+                  "loss_oracle": {k: round(v, 7) for k, v in first.items()},
+                  "rel": {k: float("%.3e" % v) for k, v in rel.items()},
+                  "max_rel": float("%.3e" % max(rel.values())), "bar": bar, "pass": bool(max(rel.values()) <= bar),
+                  "what": "eval-mode losses of the HIP engine vs the CPU oracle on the same bs=%d batch (seed 99), "
+                          "initial weights init_values(cfg, 0), gumbel noise and LPM negatives; relative error per "
+                          "loss (denominator max(|oracle|, 1e-3))" % bsz}
+    return res, parity
 
 
 def main():
@@ -406,8 +488,14 @@ def main():
                             n_triples=shape["n_triples"], npv=shape["npv"])
     batch["_label_counts"] = label_counts(batch)   # known on the host when a loader builds the batch
     T, P, R = shape["T"], shape["P"], shape["nbox"] + 1
-    probe = GemmProbe(2 * B * T + 2 * B * P, cfg.intermediate_size, cfg.hidden_size)
+    rows = 2 * B * T + 2 * B * P   # the wide text buffer
+    H, I = cfg.hidden_size, cfg.intermediate_size
+    probe = GemmProbe(rows, I, H)   # FFN1 forward
     probe.install()
+    # the dominant kernel by time: the weight-gradient walk; its launches of the text-layer weight gradients
+    # (gW[n_out, n_in] += dY^T X over the 20,992 wide rows; FFN1's 3072 x 768 x 20,992 is the largest shape)
+    wprobe = GemmProbe(I, H, rows, more=[(H, I, rows), (3 * H, H, rows), (H, H, rows)])
+    wprobe.install()
     cprobe = CoattnProbe()
     cprobe.install()
     gall = GemmAllProbe()
@@ -437,7 +525,7 @@ def main():
     # step is issued eagerly; with graph replay (a captured launch cannot be bracketed by timing events) they
     # run in PROBE_STEPS eager steps right after it (same kernels, same shapes)
     graphed = tr.graph and tr._graphs is not None and tr._graphs.graph is not None
-    probe.active = cprobe.active = not graphed
+    probe.active = wprobe.active = cprobe.active = not graphed
     t0 = time.perf_counter()
     host = 0.0
     for _ in range(args.steps):
@@ -447,7 +535,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     loss = float(out["loss"])   # the last timed step's (a replay's outputs are overwritten by the next)
-    probe.active = cprobe.active = False
+    probe.active = wprobe.active = cprobe.active = False
     per_rank = [dt]
     if use_dist:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
@@ -459,11 +547,11 @@ def main():
     if graphed:
         probe_steps = PROBE_STEPS
         mode, tr.graph = tr.graph, False
-        probe.active = cprobe.active = True
+        probe.active = wprobe.active = cprobe.active = True
         for _ in range(probe_steps):
             tr.step(batch)
         barrier()
-        probe.active = cprobe.active = False
+        probe.active = wprobe.active = cprobe.active = False
         tr.graph = mode
     # every GEMM of one eager step, after the timed region (the per-launch events would perturb the timed steps)
     mode, tr.graph = tr.graph, False
@@ -485,6 +573,13 @@ def main():
     peak = PEAK_BF16_MFMA if bf else (PEAK_F32_X6 if x6 else PEAK_F32_MFMA)
     kname = head_kernel(bf) if (bf or x6) else "gemm_f32_kernel"
     traffic, traffic_src = pmc_traffic(probe.key, kname)
+    wkname = head_wgrad_kernel(bf) if (bf or x6) else "gemm_f32_kernel"
+    w_ms = wprobe.mean_ms()
+    Mw, Nw, Kw = wprobe.key
+    w_flops = 2.0 * Mw * Nw * Kw
+    w_ach = w_flops / (w_ms * 1e-3) if w_ms else None
+    w_traffic, w_traffic_src = pmc_traffic(wprobe.key, wkname)
+    nw, w_tot_ms, w_tot_flops = wprobe.aggregate()
     ref_sample = 3.0 * ref_fwd_flops(T, P, R, shape["n_triples"])
     co_flops = 3.0 * coattn_fwd_flops(T, P, R) * B
     co_ms = cprobe.total_ms() / probe_steps if cprobe.events else None
@@ -511,19 +606,36 @@ def main():
                    "decision": tr._graphs.last_decision} if tr._graphs is not None else None),
         "loss": round(loss, 4),
         "step_mfma_frac_vs_ref_flops": round(B * ref_sample / (ms_step * 1e-3) / peak, 4),
-        "roofline": {"bound": "mfma", "kernel": "%s text-layer FFN1 %dx%dx%d" % (kname, Mg, Ng, Kg),
-                     "achieved": round(achieved / 1e12, 2) if achieved else None,
+        # the dominant kernel by time (profiles/r5e/cfg2/step_split.txt: the 256x256 weight-gradient walk, 21 % of the
+        # fp32 step; the bf16 step's largest class likewise), measured on its largest launch shape: the FFN1 weight
+        # gradient, 12 launches per step
+        "roofline": {"bound": "mfma", "kernel": "%s, FFN1 weight gradient %dx%dx%d (split-K, tn)" % (wkname, Mw, Nw, Kw),
+                     "achieved": round(w_ach / 1e12, 2) if w_ach else None,
                      "peak": peak / 1e12, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4) if achieved else None,
-                     "traffic": traffic,
-                     "avg_launch_ms": round(gemm_ms, 4) if gemm_ms else None,
-                     "launches": len(probe.events),
+                     "frac": round(w_ach / peak, 4) if w_ach else None,
+                     "traffic": w_traffic,
+                     "avg_launch_ms": round(w_ms, 4) if w_ms else None,
+                     "launches": len(wprobe.launches(wprobe.key)),
                      "probe": "HIP events, %s" % ("%d eager steps after the timed graph replays" % probe_steps if graphed
                                                   else "timed region"),
-                     "algorithmic_flops_per_launch": gemm_flops,
+                     "algorithmic_flops_per_launch": w_flops,
                      "peak_basis": ("bf16 dense MFMA" if bf else "fp32 via 6 bf16 MFMA partial products = bf16 dense "
                                     "peak / 6" if x6 else "f32 MFMA"),
-                     "traffic_unit": "HBM bytes/launch (rocprofv3 PMC, %s)" % traffic_src if traffic else None},
+                     "traffic_unit": "HBM bytes/launch (rocprofv3 PMC, %s)" % w_traffic_src if w_traffic else None,
+                     # every text-layer weight gradient on this kernel (QKV, attention output, FFN1, FFN2 x 12 layers)
+                     "class": {"launches": nw, "ms_per_step": round(w_tot_ms / probe_steps, 3) if nw else None,
+                               "achieved": round(w_tot_flops / (w_tot_ms * 1e-3) / 1e12, 2) if nw else None,
+                               "frac": round(w_tot_flops / (w_tot_ms * 1e-3) / peak, 4) if nw else None}},
+        # the FFN1 forward (bias + GELU epilogue), the roofline line of rounds 1-5
+        "roofline_ffn1": {"bound": "mfma", "kernel": "%s text-layer FFN1 %dx%dx%d" % (kname, Mg, Ng, Kg),
+                          "achieved": round(achieved / 1e12, 2) if achieved else None,
+                          "peak": peak / 1e12, "unit": "TFLOP/s",
+                          "frac": round(achieved / peak, 4) if achieved else None,
+                          "traffic": traffic,
+                          "avg_launch_ms": round(gemm_ms, 4) if gemm_ms else None,
+                          "launches": len(probe.launches(probe.key)),
+                          "algorithmic_flops_per_launch": gemm_flops,
+                          "traffic_unit": "HBM bytes/launch (rocprofv3 PMC, %s)" % traffic_src if traffic else None},
         "gemm_all": gall.summary(peak),
         "coattn": {"ms_per_step": round(co_ms, 3) if co_ms else None,
                    "algorithmic_tflop_per_step": round(co_flops / 1e12, 3),
@@ -547,7 +659,16 @@ def main():
                                              (2 if tm["comm_dtype"] == "bf16" else 4))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            res["cpu_baseline"] = cpu_baseline(cfg, shape, args.cpu_batch, args.cpu_steps)
+            gl = gpu_parity_losses(tr, cfg, shape, args.cpu_batch)
+        except Exception as e:  # noqa: BLE001 - reported, never masks the GPU result
+            gl = None
+            res["parity"] = {"error": repr(e)}
+        try:
+            # fp32: the north-star bar 1e-3; the bf16 encoder: the bar of the bf16 goldens (tests/test_gpu_parity.py)
+            res["cpu_baseline"], par = cpu_baseline(cfg, shape, args.cpu_batch, args.cpu_steps, gl,
+                                                    bar=7e-3 if bf else 1e-3)
+            if par is not None:
+                res["parity"] = par
         except Exception as e:  # baseline only; never masks the GPU result
             res["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:

@@ -79,6 +79,33 @@ def check_batch(batch, cfg, ent_neg=None, val_neg=None):
             check_range(ent_neg[ent_neg >= 0], 0, B, "ent_neg")
         if val_neg is not None and npv is not None:
             check_range(val_neg[val_neg >= 0], 0, npv, "val_neg")
+            check_val_neg(ip, val_neg)
+
+
+def item_triples(index_p):
+    """Per-item triple count: triples stop at the first j with index_p[i, j, 0] == 0 (vilbert_k3m.py:2441; the
+    rule of struct.hip count_valid)."""
+    z = (index_p[..., 0] == 0)
+    npv = index_p.shape[1]
+    first = torch.where(z.any(dim=1), z.int().argmax(dim=1), torch.full_like(z[:, 0], npv, dtype=torch.int64))
+    return first
+
+
+def check_val_neg(index_p, val_neg):
+    """A value negative of pair (i, j) names another pair of the SAME item, so it must be below that item's own triple
+    count, not only below the padded width: a negative pointing at a padding pair would make LPM read an unset row
+    (the reference samples from range(len(property_vecs[i])), vilbert_k3m.py:2489-2494).  Only the pairs LPM
+    scores (j < n) are checked."""
+    if index_p is None or val_neg.numel() == 0:
+        return
+    n = item_triples(index_p.detach().to(val_neg.device)).view(-1, 1, 1)   # [B, 1, 1]
+    j = torch.arange(val_neg.shape[1], device=val_neg.device).view(1, -1, 1)
+    scored = (j < n) & (val_neg >= 0)
+    bad = scored & (val_neg >= n)
+    if bool(bad.any()):
+        i, jj, e = [int(x) for x in bad.nonzero()[0]]
+        raise K3mIndexError("val_neg: index %d of item %d pair %d out of range [0, %d) (the item's triple count)"
+                            % (int(val_neg[i, jj, e]), i, jj, int(n.view(-1)[i])))
 
 
 def sync(name):

@@ -34,6 +34,7 @@ from . import _lib as L
 
 
 def _key(tr, batch):
+    from . import ops
     parts = []
     for k in sorted(batch):
         v = batch[k]
@@ -41,7 +42,9 @@ def _key(tr, batch):
             parts.append((k, tuple(v.shape), str(v.dtype), v.device.index))
         elif k == "_label_counts":
             parts.append((k, tuple(int(x) for x in v)))
-    return tuple(parts) + (tr.dropout, tr.overlap, tr.optimizer)
+    # the deterministic mode picks different backward kernels (ops.embed_bwd & co.): a graph captured in one mode
+    # must not be replayed in the other (ops.set_deterministic can flip it at run time)
+    return tuple(parts) + (tr.dropout, tr.overlap, tr.optimizer, bool(ops.DETERMINISTIC))
 
 
 class AdamTable(object):

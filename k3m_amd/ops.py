@@ -288,7 +288,7 @@ def small_splitk(m, n, k):
     """k-split of a small fp32 product (few 64 x 64 tiles, long k: the m = 64 pooled / gate projections, the
     389-row region-head GEMMs): one workgroup per (tile, k-slice) instead of one per tile walking all of k, the
     requested epilogue applied by the split-K reduction.  1 = no split."""
-    if not SMALL_SPLITK or m <= 8:
+    if not SMALL_SPLITK:
         return 1
     if n <= 8:
         # the skinny kernel (gemm.hip gemm_skinny_kernel, 64 rows per workgroup): k-slices of >= 128 until the
@@ -313,7 +313,9 @@ def _splitk(m, n, k, dtype=torch.float32, grouped=False):
     the 256 CUs in whole waves.  fp32 (bf16x6 kernel) tiles are 256x128 at one block per CU;
     bf16 tiles are 256x256 at one block per CU."""
     if dtype == torch.float32 and (n <= 8 or m <= 8):
-        return 1   # n <= 8: the skinny kernel, split by small_splitk inside gemm()
+        # n <= 8: the skinny kernel; m <= 8 (a one-output Linear such as struc_w2): the 64 x 64 tiles.  Both are
+        # split over k by small_splitk inside gemm(), not here (a 256-row x6 tile would be >= 97 % padding)
+        return 1
     if dtype == torch.float32 and F32_ALGO == L.F32_SPLIT_BF16X6:
         tiles = ((m + 255) // 256) * ((n + 127) // 128)
         if tiles >= 200 or k < 2048:
@@ -508,7 +510,11 @@ def set_deterministic(on=True):
 def embed_bwd(ids, tt, ds, dword, dpos, dtyp):
     nseq, ln = ids.shape
     if DETERMINISTIC:
-        assert dtyp.shape[0] == 2, "deterministic embedding backward: type_vocab_size 2"
+        # the fixed-order kernel sums the token-type rows for ids {0, 1} only (type_vocab_size 2, every config of
+        # the reference); refuse another table size instead of folding ids >= 2 into row 1 (an explicit error, not
+        # an assert that `python -O` would strip)
+        if dtyp.shape[0] != 2:
+            raise ValueError("deterministic embedding backward supports type_vocab_size 2, got %d" % dtyp.shape[0])
         ws = torch.empty((ln * 2 * dword.shape[1],), dtype=torch.float32, device=ds.device)
         call("k3m_embed_bwd_det", ptr(ids), ptr(tt), ptr(ds), ptr(dword), ptr(dpos), ptr(dtyp), nseq, ln,
              dword.shape[1], ptr(ws), dt(ds), stream())

@@ -56,7 +56,16 @@ def test_check_batch_negatives_and_lengths():
     npv = b["index_p"].shape[1]
     ent = torch.full((2, npv, 2), -1, dtype=torch.int64)
     val = torch.full((2, npv, 2), -1, dtype=torch.int64)
-    ent[0, 0, 0], val[1, 0, 1] = 1, npv - 1
+    n = int(debug.item_triples(b["index_p"])[1])   # 10 triples, padded to npv = 20 pairs
+    assert n == 10 < npv
+    ent[0, 0, 0], val[1, 0, 1] = 1, n - 1
+    debug.check_batch(b, cfg, ent, val)
+    # a value negative naming a padding pair (n <= k < npv) is refused too -- LPM would read an unset row
+    val[1, 0, 1] = n
+    with pytest.raises(debug.K3mIndexError, match="triple count"):
+        debug.check_batch(b, cfg, ent, val)
+    val[1, n, 1] = npv - 1   # pairs j >= n are not scored: their table entries are not checked
+    val[1, 0, 1] = n - 1
     debug.check_batch(b, cfg, ent, val)
     ent[0, 0, 1] = 2   # only 2 items in the batch
     with pytest.raises(debug.K3mIndexError, match="ent_neg"):

@@ -268,7 +268,7 @@ def test_dgelu_colsum_slabs(dev, dtype, m, n, k):
 
 
 @pytest.mark.parametrize("m,n,k", [(64, 768, 768), (64, 1024, 1024), (389, 1024, 2048), (389, 1024, 1601),
-                                   (100, 300, 2048)])
+                                   (100, 300, 2048), (1, 768, 640), (5, 300, 1500)])
 @pytest.mark.parametrize("epi", ["none", "bias", "gelu", "dgelu", "sigmoid", "beta"])
 def test_small_splitk_epilogues(dev, m, n, k, epi):
     """Small fp32 products split over k automatically (ops.small_splitk): the epilogue the caller
