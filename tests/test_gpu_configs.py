@@ -86,7 +86,7 @@ def test_bf16_matches_fp32_step(dev, name):
     fr = flip_rate(qf, qb)
     # how often the bf16 encoder changes the hard gumbel gate's choice (vilbert_k3m.py:2363-2372)
     print("bf16 vs fp32 %s: hard-gate flips %s" % (name, fr))
-    assert fr["all"] <= 0.05, fr
+    assert fr["all"] <= 2e-3, fr   # measured 4.5e-4 to 4.7e-4 (profiles/r6/gate_flip_rate.json)
     assert np.all(np.isfinite(lb)), lb
     rel = np.abs(lb - lf) / np.maximum(np.abs(lf), 1e-3)
     cos = float(gf @ gb / (gf.norm() * gb.norm()))
