@@ -27,7 +27,7 @@ def build(force=False, jobs=8, verbose=False):
     srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
     objdir = os.path.join(HERE, "build")
     os.makedirs(objdir, exist_ok=True)
-    deps = [os.path.join(CSRC, "common.h"), os.path.join(CSRC, "gemm_f32_tile.h"), os.path.join(CSRC, "gemm_x6_tile.h"), os.path.join(CSRC, "gemm_b16_tile.h"), os.path.join(CSRC, "flash_frag.h"), os.path.join(os.path.dirname(HERE), "include", "k3m_hip.h")]
+    deps = [os.path.join(CSRC, "common.h"), os.path.join(CSRC, "gemm_f32_tile.h"), os.path.join(CSRC, "gemm_x6_tile.h"), os.path.join(CSRC, "gemm_b16_tile.h"), os.path.join(CSRC, "gemm_b16_ws.h"), os.path.join(CSRC, "flash_frag.h"), os.path.join(os.path.dirname(HERE), "include", "k3m_hip.h")]
     dep_m = max(os.path.getmtime(d) for d in deps)
 
     def one(src):

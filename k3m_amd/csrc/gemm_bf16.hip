@@ -20,6 +20,7 @@
 
 #include "common.h"
 #include "gemm_b16_tile.h"
+#include "gemm_b16_ws.h"
 
 namespace {
 
@@ -492,6 +493,10 @@ const int kB16Dual = k3m_env_int("K3M_B16_DUAL", 2);
 // measured slower on config 3 (profiles/r5d/README.txt): off
 const int kB16PP = k3m_env_int("K3M_B16_PP", 0);
 constexpr bool dual_epi(int epi) { return epi == K3M_EPI_BIAS_GELU || epi == K3M_EPI_DGELU; }
+// K3M_B16_WS: the K-contiguous forwards with a bf16 C on the epilogue-wave kernel (gemm_b16_ws.h): bit 0 the bias+GELU
+// epilogue, bit 1 bias / none.  Needs K % 32 == 0 and K >= 32 * ws::KMIN, beta = 0, no split-K, aligned C / aux / bias.
+const int kB16WS = k3m_env_int("K3M_B16_WS", 0);
+constexpr int ws_bit(int epi) { return epi == K3M_EPI_BIAS_GELU ? 1 : (epi == K3M_EPI_BIAS || epi == K3M_EPI_NONE) ? 2 : 0; }
 
 long long nb_of(const K3mGemm& g, int bm, int bn);
 
@@ -509,8 +514,42 @@ void dual_launch(const k3m_b16::GemmGroup& grp_in, hipStream_t st) {
                      grp);
 }
 
+bool ws_ok(const k3m_b16::GemmGroup& grp) {
+  for (int i = 0; i < grp.count; ++i) {
+    const K3mGemm& g = grp.g[i];
+    if (g.splitk > 1 || g.beta != 0.f || g.k % k3m_b16::ws::BKW != 0 || g.k < k3m_b16::ws::BKW * k3m_b16::ws::KMIN ||
+        g.n < 8 || g.n % 8 != 0 || g.ldc % 8 != 0 || !aligned16(g.c))
+      return false;
+    if (g.epilogue != K3M_EPI_NONE && !aligned16(g.bias)) return false;
+    if (g.epilogue == K3M_EPI_BIAS_GELU && (g.ldaux % 8 != 0 || !aligned16(g.aux))) return false;
+    // byte offsets of the buffer stores are 32-bit
+    if (((long long)(g.m - 1) * g.ldc + g.n) * 2 >= 0x7ffffff0LL) return false;
+    if (g.epilogue == K3M_EPI_BIAS_GELU && ((long long)(g.m - 1) * g.ldaux + g.n) * 2 >= 0x7ffffff0LL) return false;
+  }
+  return true;
+}
+
+template <int EPI>
+void ws_launch(const k3m_b16::GemmGroup& grp_in, hipStream_t st) {
+  k3m_b16::GemmGroup grp = grp_in;   // units re-counted for the 256 x 128 tiles
+  int nb = 0;
+  for (int i = 0; i < grp.count; ++i) {
+    grp.start[i] = nb;
+    nb += (int)nb_of(grp.g[i], k3m_b16::ws::TBM, k3m_b16::ws::TBN);
+  }
+  grp.start[grp.count] = nb;
+  const int nblk = nb < b16_cus() ? nb : b16_cus();
+  hipLaunchKernelGGL((k3m_b16::ws::gemm_ws_kernel<EPI>), dim3(nblk), dim3(512), 0, st, grp);
+}
+
 template <int TBM, int TBN, int WM, int WN, bool AK, bool BK_, int EPI, typename CT, int MF>
 void persist_launch(const k3m_b16::GemmGroup& grp_in, hipStream_t st) {
+  if constexpr (AK && BK_ && std::is_same<CT, bf16_t>::value && ws_bit(EPI) != 0) {
+    if ((kB16WS & ws_bit(EPI)) != 0 && ws_ok(grp_in)) {
+      ws_launch<EPI>(grp_in, st);
+      return;
+    }
+  }
   if (kB16Dual == 1 || (kB16Dual == 2 && dual_epi(EPI))) {
     dual_launch<AK, BK_, EPI, CT, MF>(grp_in, st);
     return;
