@@ -27,13 +27,17 @@ def build(force=False, jobs=8, verbose=False):
     srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
     objdir = os.path.join(HERE, "build")
     os.makedirs(objdir, exist_ok=True)
-    deps = [os.path.join(CSRC, "common.h"), os.path.join(CSRC, "gemm_f32_tile.h"), os.path.join(CSRC, "gemm_x6_tile.h"), os.path.join(CSRC, "gemm_b16_tile.h"), os.path.join(CSRC, "gemm_b16_ws.h"), os.path.join(CSRC, "flash_frag.h"), os.path.join(os.path.dirname(HERE), "include", "k3m_hip.h")]
+    deps = [os.path.join(CSRC, "common.h"), os.path.join(CSRC, "gemm_f32_tile.h"), os.path.join(CSRC, "gemm_x6_tile.h"), os.path.join(CSRC, "gemm_b16_tile.h"), os.path.join(CSRC, "flash_frag.h"), os.path.join(os.path.dirname(HERE), "include", "k3m_hip.h")]
     dep_m = max(os.path.getmtime(d) for d in deps)
+
+    # headers only one translation unit includes
+    own = {"gemm_bf16.hip": [os.path.join(CSRC, "gemm_b16_ws.h")]}
 
     def one(src):
         s = os.path.join(CSRC, src)
         o = os.path.join(objdir, src + ".o")
-        if not force and os.path.exists(o) and os.path.getmtime(o) >= max(os.path.getmtime(s), dep_m):
+        dm = max([dep_m] + [os.path.getmtime(d) for d in own.get(src, [])])
+        if not force and os.path.exists(o) and os.path.getmtime(o) >= max(os.path.getmtime(s), dm):
             return o
         cmd = [hipcc()] + FLAGS + ["-c", s, "-o", o]
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -148,7 +148,6 @@ __global__ __launch_bounds__(FNT, 2) void flash_long_fwd_kernel(const uint16_t* 
       const float mref = mn == -INFINITY ? 0.f : mn;   // a row with every key so far at -inf: keep exp2 finite
       const float alpha = __builtin_amdgcn_exp2f(m2 - mref);
       m2 = mn;
-      lp *= alpha;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
       // dropout counter off + prow lk + j = cb + a compile-time offset per register (64-bit math once per chunk);
@@ -159,7 +158,7 @@ __global__ __launch_bounds__(FNT, 2) void flash_long_fwd_kernel(const uint16_t* 
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float p = __builtin_amdgcn_exp2f(S[jt][r] - mref);
-          lp += p;
+          lp = jt == 0 && r == 0 ? fmaf(lp, alpha, p) : lp + p;   // the rescale fused explicitly (fwd2 does the same)
           S[jt][r] = p * k3m_drop(dr, cb + (uint64_t)(32 * jt + (r & 3) + 8 * (r >> 2)));
         }
       // O^T += V^T P^T: A = V image read transposed in the accumulator k order, B = P from the registers
@@ -446,6 +445,433 @@ __global__ __launch_bounds__(bwd_max_waves<HD>() * 64, 1) void flash_long_bwd_ke
   }
 }
 
+// ------------------------------------------------------------------ backward, LDS-DMA form (K3M_FLASH_LONG_BWD=2)
+// The same workgroup decomposition and arithmetic as flash_long_bwd_kernel, with every operand staged by LDS-DMA
+// (global_load_lds: no staging registers, no ds_write; the images' chunk swizzle goes into the per-lane source
+// address, the XOR being an involution):
+//  * K and V images of the group: one DMA burst in the prologue (the register form waited for one HBM round trip
+//    per 640-thread pass);
+//  * query chunks (Q rows, dO rows, raw LSE and D) in a ring of NQB slots, the DMA of chunk c + NQB issued as soon
+//    as chunk c's key phase has read its slot: NQB - 1 chunks in flight instead of one register-prefetched chunk;
+//  * rows past lq / lk are clamped copies of valid rows instead of zeros: their P (LSE = +inf, key mask -inf) and
+//    hence Pd and dS are exactly 0, so every sum is unchanged (bit-identical to the register form);
+//  * dQ leaves by buffer stores (rows past lq dropped by the descriptor), so each wave's vector-memory count per
+//    chunk is fixed and the DMA waits are counted (vmcnt), two barriers per chunk instead of three.
+template <int NC>
+__device__ __forceinline__ int swz_of(int r) {
+  if constexpr (NC == 16) return ((r & 3) << 2) | ((r >> 2) & 3);
+  else return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);   // NC == 8
+}
+
+// One LDS-DMA wave instruction as inline asm (as gemm_x6p.hip PPDLoop): issued through the builtin, the compiler's
+// waitcnt pass cannot tell the ring slots from the K / V / dS^T images and puts a vmcnt(0) before every later LDS
+// access, i.e. drains the chunks meant to stay in flight.  Hidden from it, the DMAs are ordered only by the counted
+// vmcnt waits below (its own vmcnt counts for other loads stay conservative).  M0 = the wave-uniform LDS destination;
+// s_nop 0: the M0 write -> LDS-DMA hazard.
+__device__ __forceinline__ uint32_t lds_addr(const void* lds) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds);
+}
+__device__ __forceinline__ void lds_dma16(const void* g, void* lds) {
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(lds_addr(lds)) : "memory");
+}
+__device__ __forceinline__ void lds_dma4(const void* g, void* lds) {
+  asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "{m0}"(lds_addr(lds)) : "memory");
+}
+
+// vmcnt(n), n wave-uniform (a scalar switch over the immediate forms)
+template <int N>
+__device__ __forceinline__ void vmwait() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+__device__ __forceinline__ void vmwait_n(int n) {
+  switch (n < 0 ? 0 : n) {
+#define K3M_FL_W(N) case N: vmwait<N>(); break;
+    K3M_FL_W(0) K3M_FL_W(1) K3M_FL_W(2) K3M_FL_W(3) K3M_FL_W(4) K3M_FL_W(5) K3M_FL_W(6) K3M_FL_W(7)
+    K3M_FL_W(8) K3M_FL_W(9) K3M_FL_W(10) K3M_FL_W(11) K3M_FL_W(12) K3M_FL_W(13) K3M_FL_W(14) K3M_FL_W(15)
+    K3M_FL_W(16) K3M_FL_W(17) K3M_FL_W(18) K3M_FL_W(19) K3M_FL_W(20) K3M_FL_W(21) K3M_FL_W(22) K3M_FL_W(23)
+    K3M_FL_W(24) K3M_FL_W(25) K3M_FL_W(26) K3M_FL_W(27) K3M_FL_W(28) K3M_FL_W(29) K3M_FL_W(30) K3M_FL_W(31)
+    K3M_FL_W(32) K3M_FL_W(33) K3M_FL_W(34) K3M_FL_W(35) K3M_FL_W(36) K3M_FL_W(37) K3M_FL_W(38) K3M_FL_W(39)
+    K3M_FL_W(40) K3M_FL_W(41) K3M_FL_W(42) K3M_FL_W(43) K3M_FL_W(44) K3M_FL_W(45) K3M_FL_W(46) K3M_FL_W(47)
+#undef K3M_FL_W
+    default: vmwait<0>(); break;
+  }
+}
+
+// one DMA instruction (1 KiB: 1024 / (2 HW) rows) of an [rows][HW] image at rows r0 .. : lane -> (row, slot), the
+// chunk stored in that slot read from row min(row, nvalid - 1) of the global operand (chunks past the head: clamped,
+// never read).  saddr + 32-bit voffset form: the wave-uniform 64-bit base (the operand's row 0 + head offset) stays
+// in SGPRs and each lane keeps one offset register (64-bit per-lane pointers had the forward spill in its loop).
+template <int NC, int NCL>
+__device__ __forceinline__ void dma_rows(uint16_t* img, int r0, const uint16_t* __restrict__ g, long long ld,
+                                         long long row0, int nvalid, int hoff, int lane) {
+  const int rr = lane / NC, slot = lane % NC, r = r0 + rr;   // 64 / NC rows per instruction
+  const int c = min(slot ^ swz_of<NC>(r), NCL - 1);
+  const uint16_t* base = g + row0 * ld + hoff;
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  // (readfirstlane returns int: through uint32_t, or the low word's sign would spread into the high word)
+  const uint64_t bu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                      (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t voff = (uint32_t)(((long long)min(r, nvalid - 1) * ld + 8 * c) * 2);
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(bu), "{m0}"(lds_addr(img + r0 * NC * 8))
+               : "memory");
+}
+
+template <int HD>
+__global__ __launch_bounds__(bwd_max_waves<HD>() * 64, 1) void flash_long_bwd2_kernel(
+    const uint16_t* __restrict__ dctx, long long ldc, const uint16_t* __restrict__ q, long long ldq,
+    const uint16_t* __restrict__ k, long long ldk, const uint16_t* __restrict__ v, long long ldv,
+    const float* __restrict__ kmask, const float* __restrict__ lse, const float* __restrict__ dvec,
+    uint16_t* __restrict__ dq, uint16_t* __restrict__ dk, uint16_t* __restrict__ dv, long long lddq, long long lddk,
+    long long lddv, float* __restrict__ dq_ws, int lq, int lk, int nh, int tpg, int nqb, float scale, float p_drop,
+    uint64_t seed, uint64_t off) {
+  using G = Geo<HD>;
+  constexpr int NCL = G::NCL, NC = G::NC, HW = G::HW, DT = G::DT, KS = G::KS;
+  constexpr int RPI = 64 / NC;                 // image rows per DMA instruction
+  constexpr int NQI = BQC / RPI;               // DMA instructions per chunk operand (Q or dO)
+  constexpr int NCI = 2 * NQI + 1;             // per chunk, + one dword instruction for (LSE, D)
+  constexpr int SL = 2 * BQC * HW + 128;       // bf16 elements per ring slot (+ 64 floats)
+  constexpr int NT16 = 2 * (HD / 16);          // 16 x 16 dQ tiles of a 32-query chunk
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int nw = blockDim.x >> 6;
+  const int GK = 32 * nw;
+  uint16_t* Kimg = smem;                       // [GK][HW]
+  uint16_t* Vimg = Kimg + GK * HW;             // [GK][HW]
+  uint16_t* dSt = Vimg + GK * HW;              // [GK][BQC]
+  uint16_t* ring = dSt + GK * BQC;             // nqb x {Q [BQC][HW], dO [BQC][HW], LSE [32] f32, D [32] f32}
+  const int s = blockIdx.x / nh, h = blockIdx.x % nh, grp = blockIdx.y, ngrp = gridDim.y;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
+  const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
+  const int hoff = h * HD;
+  const long long lrow0 = ((long long)s * nh + h) * lq;
+  const K3mDrop dr = k3m_drop_init(seed, p_drop);
+  const float sl2 = scale * LOG2E;
+  const int NKT = (lk + 31) >> 5;
+  const int kt0 = grp * tpg, nkt = min(tpg, NKT - kt0);
+  const int kg0 = 32 * kt0;
+  const int NQC = (lq + BQC - 1) / BQC;
+  const bool kw = w < nkt;
+  const int jl = 32 * w + cl, j = kg0 + jl;
+  const bool jv = kw && j < lk;
+  const float mj2 = jv ? (kmask ? kmask[krow0 + j] * LOG2E : 0.f) : -INFINITY;
+  // this wave's share of every chunk's DMA (instruction i by wave i % nw) and of the dQ tiles (tile t by t % nw)
+  const int n_w = w < NCI ? (NCI - 1 - w) / nw + 1 : 0;
+  const int t_w = w < NT16 ? (NT16 - 1 - w) / nw + 1 : 0;
+  const int st_w = 4 * t_w;   // dQ buffer stores per chunk
+  auto dma_chunk = [&](int c) {
+    uint16_t* sl = ring + (c % nqb) * SL;
+    const int q0 = c * BQC;
+    for (int i = w; i < NCI; i += nw) {
+      if (i < NQI) dma_rows<NC, NCL>(sl, i * RPI, q, ldq, qrow0 + q0, lq - q0, hoff, lane);
+      else if (i < 2 * NQI) dma_rows<NC, NCL>(sl + BQC * HW, (i - NQI) * RPI, dctx, ldc, qrow0 + q0, lq - q0, hoff, lane);
+      else {   // raw LSE (lanes 0-31) and D (lanes 32-63) of the chunk's rows, clamped
+        const long long lr = lrow0 + min(q0 + cl, lq - 1);
+        lds_dma4(kl ? dvec + lr : lse + lr, sl + 2 * BQC * HW);
+      }
+    }
+  };
+  // prologue: the group's K and V images (rows past lk or past the group: clamped copies), then the first chunks
+  {
+    const int kv_inst = GK / RPI;   // per image; a multiple of nw
+    for (int i = w; i < kv_inst; i += nw) {
+      dma_rows<NC, NCL>(Kimg, i * RPI, k, ldk, krow0 + kg0, lk - kg0, hoff, lane);
+      dma_rows<NC, NCL>(Vimg, i * RPI, v, ldv, krow0 + kg0, lk - kg0, hoff, lane);
+    }
+  }
+  const int npre = min(nqb, NQC);
+  for (int c = 0; c < npre; ++c) dma_chunk(c);
+  vmwait_n(n_w * (npre - 1));   // K, V and chunk 0 landed (raw barrier: __syncthreads would drain every DMA)
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  floatx16 dV[DT], dK[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    dV[dt] = zero16();
+    dK[dt] = zero16();
+  }
+  const long long dqbytes = ngrp == 1 ? ((long long)(gridDim.x / nh) * lq - 1) * lddq * 2 + (long long)nh * HD * 2
+                                      : (long long)ngrp * gridDim.x * lq * HD * 4;
+  const __amdgpu_buffer_rsrc_t rdq = __builtin_amdgcn_make_buffer_rsrc(
+      ngrp == 1 ? (void*)dq : (void*)dq_ws, (short)0, (int)min(dqbytes, 0x7ffffff0LL), 0x00020000);
+  for (int c = 0; c < NQC; ++c) {
+    const int q0 = c * BQC;
+    const uint16_t* Qc = ring + (c % nqb) * SL;
+    const uint16_t* dOc = Qc + BQC * HW;
+    const float* Lc = reinterpret_cast<const float*>(dOc + BQC * HW);
+    const float* Dc = Lc + BQC;
+    // ---- key phase (as flash_long_bwd_kernel; LSE scaled and padding rows set to +inf here)
+    if (kw) {
+      uint32_t keep = 0xffffu;
+      if (dr.thr != 0u) {
+        const uint64_t cb = off + (uint64_t)(lrow0 + q0 + 4 * kl) * (uint64_t)lk + (uint64_t)j;
+        keep = 0u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          keep |= (uint32_t)((k3m_hash_key(dr.key, cb + (uint64_t)((8 * (r >> 2) + (r & 3)) * lk)) >> 8) >= dr.thr) << r;
+      }
+      floatx16 S = zero16(), dP = zero16();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        S = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag<NC>(Qc, 0, ks, lane), rowfrag<NC>(Kimg, 32 * w, ks, lane), S,
+                                                    0, 0, 0);
+        dP = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag<NC>(dOc, 0, ks, lane), rowfrag<NC>(Vimg, 32 * w, ks, lane),
+                                                     dP, 0, 0, 0);
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int i0 = 8 * a + 4 * kl;
+        const float4 l4 = *reinterpret_cast<const float4*>(Lc + i0);
+        const float4 d4 = *reinterpret_cast<const float4*>(Dc + i0);
+        const float lraw[4] = {l4.x, l4.y, l4.z, l4.w}, dvv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int r = 4 * a + b;
+          const float lvb = q0 + i0 + b < lq ? lraw[b] * LOG2E : INFINITY;   // padding query rows: P = 0
+          const float p = __builtin_amdgcn_exp2f(fmaf(S[r], sl2, mj2) - lvb);
+          const float dm = (keep >> r) & 1u ? dr.scale : 0.f;
+          S[r] = p * dm;
+          dP[r] = p * (dP[r] * dm - dvv[b]);
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 bp = accfrag(S, s2), bs = accfrag(dP, s2);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          dV[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag<NC, true>(dOc, 16 * s2, 32 * dt, lane), bp, dV[dt], 0, 0, 0);
+          dK[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag<NC, true>(Qc, 16 * s2, 32 * dt, lane), bs, dK[dt], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        uint2 wd;
+        wd.x = bf_bits(dP[4 * a]) | ((uint32_t)bf_bits(dP[4 * a + 1]) << 16);
+        wd.y = bf_bits(dP[4 * a + 2]) | ((uint32_t)bf_bits(dP[4 * a + 3]) << 16);
+        *reinterpret_cast<uint2*>(dSt + ioff<4>(jl, a) + 4 * kl) = wd;
+      }
+    } else {
+#pragma unroll
+      for (int a = 0; a < 4; ++a) *reinterpret_cast<uint2*>(dSt + ioff<4>(jl, a) + 4 * kl) = make_uint2(0u, 0u);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // dS^T complete; every read of this chunk's slot done
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- dQ phase: 16 x 16 tiles dealt to the waves; 4 buffer stores per tile, rows past lq dropped
+    for (int t = w; t < NT16; t += nw) {
+      const int qt = t & 1, d16 = t >> 1;
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      int kt = 0;
+      for (; kt + 1 < nkt; kt += 2) {
+        const bf16x8 a0 = trfrag16<4>(dSt, 32 * kt, 16 * qt, lane), b0 = trfrag16<NC>(Kimg, 32 * kt, 16 * d16, lane);
+        const bf16x8 a1 = trfrag16<4>(dSt, 32 * kt + 32, 16 * qt, lane);
+        const bf16x8 b1 = trfrag16<NC>(Kimg, 32 * kt + 32, 16 * d16, lane);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc, 0, 0, 0);
+      }
+      if (kt < nkt)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag16<4>(dSt, 32 * kt, 16 * qt, lane),
+                                                      trfrag16<NC>(Kimg, 32 * kt, 16 * d16, lane), acc, 0, 0, 0);
+      const int dd = 16 * d16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ii = q0 + 16 * qt + 4 * (lane >> 4) + r;
+        if (ngrp == 1) {
+          const int o = ii < lq ? (int)(((qrow0 + ii) * lddq + hoff + dd) * 2) : 0x7fffffff;
+          __builtin_amdgcn_raw_buffer_store_b16(bf_bits(acc[r] * scale), rdq, o, 0, 0);
+        } else {
+          const int o = ii < lq ? (int)(((((long long)grp * gridDim.x + blockIdx.x) * lq + ii) * HD + dd) * 4)
+                                : 0x7fffffff;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[r]), rdq, o, 0, 0);
+        }
+      }
+    }
+    // ---- the next chunks: chunk c + nqb into this chunk's slot; chunk c + 1 must have landed before the barrier
+    const bool more = c + nqb < NQC;
+    if (more) dma_chunk(c + nqb);
+    if (c + 1 < NQC) {
+      // vector-memory operations this wave issued after chunk c + 1's DMA: chunks x in [c + 2 - nqb, c] each
+      // stored st_w dQ values and issued n_w DMAs when x + nqb < NQC; a prologue DMA also has the later prologue
+      // chunks after it
+      int younger = 0;
+      const int x0 = c + 2 - nqb;
+      for (int x = x0 < 0 ? 0 : x0; x <= c; ++x) younger += st_w + (x + nqb < NQC ? n_w : 0);
+      if (c + 1 < nqb) younger += n_w * (npre - 1 - (c + 1));
+      vmwait_n(younger);
+    }
+    __builtin_amdgcn_s_barrier();   // chunk c + 1 visible; dS^T free
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (jv) {
+    uint16_t* pv = dv + (krow0 + j) * lddv + hoff + 4 * kl;
+    uint16_t* pk = dk + (krow0 + j) * lddk + hoff + 4 * kl;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        uint2 wv, wk;
+        wv.x = bf_bits(dV[dt][4 * a]) | ((uint32_t)bf_bits(dV[dt][4 * a + 1]) << 16);
+        wv.y = bf_bits(dV[dt][4 * a + 2]) | ((uint32_t)bf_bits(dV[dt][4 * a + 3]) << 16);
+        wk.x = bf_bits(dK[dt][4 * a] * scale) | ((uint32_t)bf_bits(dK[dt][4 * a + 1] * scale) << 16);
+        wk.y = bf_bits(dK[dt][4 * a + 2] * scale) | ((uint32_t)bf_bits(dK[dt][4 * a + 3] * scale) << 16);
+        *reinterpret_cast<uint2*>(pv + 32 * dt + 8 * a) = wv;
+        *reinterpret_cast<uint2*>(pk + 32 * dt + 8 * a) = wk;
+      }
+  }
+}
+
+// ------------------------------------------------------------------ forward, LDS-DMA form (K3M_FLASH_LONG_FWD=2)
+// flash_long_fwd_kernel with the K / V chunks staged by LDS-DMA into a ring of NKB slots (chunk c + NKB - 1 issued
+// right after the barrier that retires chunk c - 1's slot, so NKB - 1 chunks are in flight instead of one
+// register-prefetched chunk, and no staging registers: at d = 64 three workgroups fit a CU instead of two).  Keys
+// past lk are clamped copies instead of zeros; their scores carry the -inf key mask either way, so P, the running
+// max / sum and the context are bit-identical.
+template <int HD> constexpr int fwd2_nkb() { return HD == 64 ? 3 : 2; }
+template <int HD> constexpr int fwd2_occ() { return HD == 64 ? 3 : 2; }
+
+template <int HD>
+__global__ __launch_bounds__(FNT, fwd2_occ<HD>()) void flash_long_fwd2_kernel(
+    const uint16_t* __restrict__ q, long long ldq, const uint16_t* __restrict__ k, long long ldk,
+    const uint16_t* __restrict__ v, long long ldv, const float* __restrict__ kmask, uint16_t* __restrict__ ctx,
+    long long ldc, float* __restrict__ lse, int lq, int lk, int nh, float scale, float p_drop, uint64_t seed,
+    uint64_t off) {
+  using G = Geo<HD>;
+  constexpr int NCL = G::NCL, NC = G::NC, HW = G::HW, DT = G::DT, KS = G::KS;
+  constexpr int NKB = fwd2_nkb<HD>();
+  constexpr int RPI = 64 / NC;                 // image rows per DMA instruction
+  constexpr int CI = FKC / RPI;                // DMA instructions per chunk and operand
+  constexpr int NWF = FNT / 64;                // 4 waves
+  constexpr int N_W = 2 * CI / NWF;            // DMA instructions per wave per chunk
+  static_assert((2 * CI) % NWF == 0, "chunk DMA must split over the waves");
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* ring = smem;                                            // NKB x {K [FKC][HW], V [FKC][HW]}
+  float* msk = reinterpret_cast<float*>(ring + NKB * 2 * FKC * HW);   // [LKP] mask * log2 e, -inf past lk
+  const int s = blockIdx.x / nh, h = blockIdx.x % nh;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
+  const int nkc = (lk + FKC - 1) / FKC, LKP = nkc * FKC;
+  const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
+  const int hoff = h * HD;
+  const int qw0 = blockIdx.y * (FNT / 2) + 32 * w;
+  const bool wact = qw0 < lq;
+  const int i = qw0 + cl;
+  const bool iv = i < lq;
+  const K3mDrop dr = k3m_drop_init(seed, p_drop);
+  const float sl2 = scale * LOG2E;
+  const long long prow = ((long long)s * nh + h) * lq + min(i, lq - 1);
+  auto dma_chunk = [&](int c) {   // K and V rows c FKC .. + FKC - 1 (clamped) into slot c % NKB
+    uint16_t* Kb = ring + (c % NKB) * 2 * FKC * HW;
+#pragma unroll
+    for (int t = 0; t < N_W; ++t) {
+      const int inst = w + NWF * t;   // 0 .. 2 CI - 1: K first, then V
+      if (inst < CI) dma_rows<NC, NCL>(Kb, inst * RPI, k, ldk, krow0 + c * FKC, lk - c * FKC, hoff, lane);
+      else dma_rows<NC, NCL>(Kb + FKC * HW, (inst - CI) * RPI, v, ldv, krow0 + c * FKC, lk - c * FKC, hoff, lane);
+    }
+  };
+  const int npre = min(NKB - 1, nkc);
+  for (int c = 0; c < npre; ++c) dma_chunk(c);
+  bf16x8 qf[KS];
+  {
+    const uint16_t* qp = q + (qrow0 + min(i, lq - 1)) * ldq + hoff + 8 * kl;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = __builtin_bit_cast(bf16x8, keep_if(iv, *reinterpret_cast<const uint4*>(qp + 16 * ks)));
+  }
+  for (int t = threadIdx.x; t < LKP; t += FNT)
+    msk[t] = t < lk ? (kmask ? kmask[krow0 + t] * LOG2E : 0.f) : -INFINITY;
+
+  floatx16 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = zero16();
+  float m2 = -INFINITY, lp = 0.f;
+  for (int c = 0; c < nkc; ++c) {
+    // chunk c landed (chunks c + 1 .. c + NKB - 2 may stay in flight), then the barrier that also retires every
+    // read of chunk c - 1's slot, which chunk c + NKB - 1 then refills
+    vmwait_n(N_W * max(0, min(NKB - 2, nkc - 1 - c)));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + NKB - 1 < nkc) dma_chunk(c + NKB - 1);
+    if (wact) {
+      const uint16_t* Kb = ring + (c % NKB) * 2 * FKC * HW;
+      const uint16_t* Vb = Kb + FKC * HW;
+      floatx16 S[FKC / 32];
+#pragma unroll
+      for (int jt = 0; jt < FKC / 32; ++jt) {
+        floatx16 a = zero16();
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag<NC>(Kb, 32 * jt, ks, lane), qf[ks], a, 0, 0, 0);
+        S[jt] = a;
+      }
+      float mc = -INFINITY;
+#pragma unroll
+      for (int jt = 0; jt < FKC / 32; ++jt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int j = c * FKC + 32 * jt + (r & 3) + 8 * (r >> 2) + 4 * kl;
+          const float x = fmaf(S[jt][r], sl2, msk[j]);
+          S[jt][r] = x;
+          mc = fmaxf(mc, x);
+        }
+      mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+      const float mn = fmaxf(m2, mc);
+      const float mref = mn == -INFINITY ? 0.f : mn;
+      const float alpha = __builtin_amdgcn_exp2f(m2 - mref);
+      m2 = mn;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+      const uint64_t cb = off + (uint64_t)prow * (uint64_t)lk + (uint64_t)(c * FKC + 4 * kl);
+      // the p = 0 test hoisted out of the element loop (k3m_drop's per-element branch): same values
+      if (dr.thr != 0u) {
+#pragma unroll
+        for (int jt = 0; jt < FKC / 32; ++jt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float p = __builtin_amdgcn_exp2f(S[jt][r] - mref);
+            lp = jt == 0 && r == 0 ? fmaf(lp, alpha, p) : lp + p;
+            const uint32_t hh = k3m_hash_key(dr.key, cb + (uint64_t)(32 * jt + (r & 3) + 8 * (r >> 2)));
+            S[jt][r] = p * ((hh >> 8) >= dr.thr ? dr.scale : 0.f);
+          }
+      } else {
+#pragma unroll
+        for (int jt = 0; jt < FKC / 32; ++jt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float p = __builtin_amdgcn_exp2f(S[jt][r] - mref);
+            lp = jt == 0 && r == 0 ? fmaf(lp, alpha, p) : lp + p;
+            S[jt][r] = p;
+          }
+      }
+#pragma unroll
+      for (int jt = 0; jt < FKC / 32; ++jt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 b = accfrag(S[jt], s2);
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt)
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag<NC, true>(Vb, 32 * jt + 16 * s2, 32 * dt, lane), b,
+                                                             o[dt], 0, 0, 0);
+        }
+    }
+  }
+  if (!wact) return;
+  const float lt = lp + __shfl_xor(lp, 32, 64);
+  const float inv = 1.f / lt;
+  if (kl == 0 && iv) lse[prow] = m2 * LN2 + __logf(lt);
+  if (iv) {
+    uint16_t* op = ctx + (qrow0 + i) * ldc + hoff + 4 * kl;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        uint2 wv;
+        wv.x = bf_bits(o[dt][4 * a] * inv) | ((uint32_t)bf_bits(o[dt][4 * a + 1] * inv) << 16);
+        wv.y = bf_bits(o[dt][4 * a + 2] * inv) | ((uint32_t)bf_bits(o[dt][4 * a + 3] * inv) << 16);
+        *reinterpret_cast<uint2*>(op + 32 * dt + 8 * a) = wv;
+      }
+  }
+}
+
 // dq = bf16(scale * sum_g ws[g]), summed in group order; one thread per 4 head dims of a query row
 __global__ __launch_bounds__(256) void flash_long_dq_reduce_kernel(const float* __restrict__ ws, uint16_t* __restrict__ dq,
                                                                    long long lddq, int nseq, int lq, int nh, int hd,
@@ -481,6 +907,15 @@ size_t fwd_lds(int lk, int hd) {
   return 2 * (4 * FKC * HW) + 4 * LKP;
 }
 
+size_t fwd2_lds(int lk, int hd) {
+  const size_t HW = hd == 96 ? 128 : hd;
+  const size_t LKP = (lk + FKC - 1) / FKC * FKC;
+  const size_t nkb = hd == 64 ? 3 : 2;
+  return nkb * 2 * FKC * HW * 2 + 4 * LKP;
+}
+// K3M_FLASH_LONG_FWD: 2 (default) the LDS-DMA forward (flash_long_fwd2_kernel), 1 the register-staged one
+const int kFlashLongFwd = k3m_env_int("K3M_FLASH_LONG_FWD", 2);
+
 // key tiles per group and groups of a head's backward
 void bwd_groups(int lk, int hd, int& tpg, int& ngrp, int& nw) {
   const int nkt = (lk + 31) / 32;
@@ -489,6 +924,15 @@ void bwd_groups(int lk, int hd, int& tpg, int& ngrp, int& nw) {
   tpg = (nkt + ngrp - 1) / ngrp;
   nw = std::max(tpg, BMIN_W);
 }
+
+// LDS bytes of flash_long_bwd2_kernel with nqb ring slots
+size_t bwd2_lds(int hd, int nw, int nqb) {
+  const size_t HW = hd == 96 ? 128 : hd, GK = 32 * (size_t)nw;
+  return 2 * (2 * GK * HW + GK * BQC) + (size_t)nqb * 2 * (2 * BQC * HW + 128);
+}
+
+// K3M_FLASH_LONG_BWD: 2 (default) the LDS-DMA backward (flash_long_bwd2_kernel), 1 the register-staged one
+const int kFlashLongBwd = k3m_env_int("K3M_FLASH_LONG_BWD", 2);
 
 size_t bwd_lds(int hd, int nw) {
   const size_t HW = hd == 96 ? 128 : hd, GK = 32 * (size_t)nw;
@@ -504,6 +948,12 @@ void set_attrs() {
     (void)hipFuncSetAttribute((const void*)flash_long_bwd_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_long_bwd_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_long_bwd_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_bwd2_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_fwd2_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_fwd2_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_fwd2_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_bwd2_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_bwd2_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     done = true;
   }
 }
@@ -524,6 +974,19 @@ extern "C" int k3m_flash_attn_long_fwd(const void* q, long long ldq, const void*
   K3M_ARG(lds <= (size_t)LDS_MAX);
   set_attrs();
   const dim3 grid(nseq * nh, (lq + FNT / 2 - 1) / (FNT / 2));
+  if (kFlashLongFwd == 2 && fwd2_lds(lk, hd) <= (size_t)LDS_MAX) {
+    const size_t lds2 = fwd2_lds(lk, hd);
+#define K3M_FL_FWD2(HD_)                                                                                          \
+    hipLaunchKernelGGL(flash_long_fwd2_kernel<HD_>, grid, dim3(FNT), lds2, st, (const uint16_t*)q, ldq,          \
+                       (const uint16_t*)k, ldk, (const uint16_t*)v, ldv, kmask, (uint16_t*)ctx, ldc, lse, lq, lk, nh, \
+                       scale, p_drop, seed, off)
+    if (hd == 64) K3M_FL_FWD2(64);
+    else if (hd == 96) K3M_FL_FWD2(96);
+    else K3M_FL_FWD2(128);
+#undef K3M_FL_FWD2
+    K3M_CHECK_LAUNCH();
+    return 0;
+  }
 #define K3M_FL_FWD(HD_)                                                                                           \
   hipLaunchKernelGGL(flash_long_fwd_kernel<HD_>, grid, dim3(FNT), lds, st, (const uint16_t*)q, ldq,                \
                      (const uint16_t*)k, ldk, (const uint16_t*)v, ldv, kmask, (uint16_t*)ctx, ldc, lse, lq, lk, nh, \
@@ -583,6 +1046,23 @@ extern "C" int k3m_flash_attn_long_bwd(const void* dctx, long long ldc, const vo
     hipLaunchKernelGGL(flash_long_prep_kernel<16>, dim3(k3m_cdiv(rows * 16, 256)), dim3(256), 0, st,
                        (const uint16_t*)dctx, ldc, (const uint16_t*)o, ldo, dvec, nseq, lq, nh, hd);
   const dim3 grid(nseq * nh, ngrp);
+  if (kFlashLongBwd == 2) {
+    const int nqb = bwd2_lds(hd, nw, 3) <= (size_t)LDS_MAX ? 3 : 2;
+    const size_t lds2 = bwd2_lds(hd, nw, nqb);
+    K3M_ARG(lds2 <= (size_t)LDS_MAX);
+    // 32-bit byte offsets of the dQ buffer stores
+    K3M_ARG(ngrp > 1 ? (long long)ngrp * rows * hd * 4 < 0x7ffffff0LL
+                     : ((long long)nseq * lq) * lddq * 2 < 0x7ffffff0LL);
+#define K3M_FL_BWD2(HD_)                                                                                          \
+    hipLaunchKernelGGL(flash_long_bwd2_kernel<HD_>, grid, dim3(64 * nw), lds2, st, (const uint16_t*)dctx, ldc,      \
+                       (const uint16_t*)q, ldq, (const uint16_t*)k, ldk, (const uint16_t*)v, ldv, kmask, lse, dvec, \
+                       (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, lddq, lddk, lddv, dq_ws, lq, lk, nh, tpg, nqb,    \
+                       scale, p_drop, seed, off)
+    if (hd == 64) K3M_FL_BWD2(64);
+    else if (hd == 96) K3M_FL_BWD2(96);
+    else K3M_FL_BWD2(128);
+#undef K3M_FL_BWD2
+  } else {
 #define K3M_FL_BWD(HD_)                                                                                          \
   hipLaunchKernelGGL(flash_long_bwd_kernel<HD_>, grid, dim3(64 * nw), lds, st, (const uint16_t*)dctx, ldc,        \
                      (const uint16_t*)q, ldq, (const uint16_t*)k, ldk, (const uint16_t*)v, ldv, kmask, lse, dvec, \
@@ -592,6 +1072,7 @@ extern "C" int k3m_flash_attn_long_bwd(const void* dctx, long long ldc, const vo
   else if (hd == 96) K3M_FL_BWD(96);
   else K3M_FL_BWD(128);
 #undef K3M_FL_BWD
+  }
   K3M_CHECK_LAUNCH();
   if (ngrp > 1) {
     hipLaunchKernelGGL(flash_long_dq_reduce_kernel, dim3(k3m_cdiv(rows * hd / 4, 256)), dim3(256), 0, st, dq_ws,

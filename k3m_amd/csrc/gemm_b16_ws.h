@@ -75,6 +75,16 @@ __device__ __forceinline__ void vm_wait() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
+// vmcnt(n) for a wave-uniform n <= 2 (NI_E + 2): a scalar switch over immediate forms
+__device__ __forceinline__ void vm_wait_n(int n) {
+  switch (n) {
+#define K3M_WS_W(N) case N: vm_wait<N>(); break;
+    K3M_WS_W(0) K3M_WS_W(1) K3M_WS_W(2) K3M_WS_W(3) K3M_WS_W(4) K3M_WS_W(5) K3M_WS_W(6) K3M_WS_W(7) K3M_WS_W(8)
+    K3M_WS_W(9) K3M_WS_W(10) K3M_WS_W(11) K3M_WS_W(12) K3M_WS_W(13) K3M_WS_W(14) K3M_WS_W(15) K3M_WS_W(16)
+#undef K3M_WS_W
+    default: vm_wait<0>(); break;
+  }
+}
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, long long bytes) {
   const int n = bytes > 0x7ffffff0LL ? 0x7ffffff0 : (int)bytes;
@@ -160,10 +170,9 @@ __device__ __forceinline__ void mfma_role(const GemmGroup& grp, uint16_t* smem, 
           }
         }
       }
-      // the last two fragment reads may stay in flight across the barrier (their stage is rewritten two barriers
-      // later; the MFMAs that use them wait for them); LDS operations complete in order, so this also retires the
-      // previous hand-off's image writes before the epilogue waves read them
-      asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+      // every fragment read of k-step gs + 1 done: its stage is rewritten right after the next barrier (DMA of
+      // k-step gs + 5); this also retires the previous hand-off's image writes before the epilogue waves read them
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -257,12 +266,12 @@ __device__ __forceinline__ void epi_role(const GemmGroup& grp, uint16_t* smem, c
   dinit();
   dma();
   dma();
-  const bool third = dma();
-  if (third) vm_wait<NI_E>();   // k-steps 0 and 1 landed, 2 in flight
-  else vm_wait<0>();
+  const int pro = (dma() ? 1 : 0) + (dma() ? 1 : 0);
+  vm_wait_n(pro * NI_E);   // k-steps 0 and 1 landed, 2 and 3 in flight
   __builtin_amdgcn_s_barrier();   // B0
   __builtin_amdgcn_sched_barrier(0);
   int pu = -1;   // the previous tile (its image is in LDS)
+  int prev_ops = pro == 2 ? NI_E : 0;   // vector-memory operations of the last step issued after its DMA wait point
   PUnit<TBM, TBN, 2, 2> prev;
   for (int u = blockIdx.x; u < total; u += P) {
     PUnit<TBM, TBN, 2, 2> cur;
@@ -272,17 +281,14 @@ __device__ __forceinline__ void epi_role(const GemmGroup& grp, uint16_t* smem, c
       // 1. a chunk of the previous tile: image read-back, epilogue, stores
       const int c = pu >= 0 ? chunk_at(ls, nk) : -1;
       if (c >= 0) epi_chunk<EPI>(grp.g[prev.p], prev.m0, prev.n0, outb, c, e, lane);
-      // 2. k-step gs + 3 into the stage k-step gs - 1 left (its fragments were read before the last barrier)
+      // 2. k-step gs + 4 into the stage of k-step gs (its fragments were read, and waited for, before the last
+      //    barrier): three k-steps in flight
       const bool d = dma();
       // 3. k-step gs + 2 must have landed before the barrier (it is read in the next k-step): the operations
-      //    issued after it are this step's stores and DMA
-      if (c >= 0) {
-        if (d) vm_wait<SPC + NI_E>();
-        else vm_wait<SPC>();
-      } else {
-        if (d) vm_wait<NI_E>();
-        else vm_wait<0>();
-      }
+      //    issued after it are the last step's and this step's stores and DMAs
+      const int younger = prev_ops + (c >= 0 ? SPC : 0) + (d ? NI_E : 0);
+      vm_wait_n(younger);
+      prev_ops = (c >= 0 ? SPC : 0) + (d ? NI_E : 0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);

@@ -83,6 +83,8 @@ if __name__ == "__main__":
     dts = {"fp32": [torch.float32], "bf16": [torch.bfloat16], "both": [torch.float32, torch.bfloat16]}[
         sys.argv[1] if len(sys.argv) > 1 else "both"]
     shapes = SHAPES5 if len(sys.argv) > 2 and sys.argv[2] == "cfg5" else SHAPES
+    if len(sys.argv) > 3:   # one shape by name
+        shapes = [sh for sh in shapes if sh[0] == sys.argv[3]]
     for d in dts:
         for sh in shapes:
             run(*sh, dtype=d)

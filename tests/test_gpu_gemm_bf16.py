@@ -376,3 +376,61 @@ def test_flash_long_d96_matches_fixed_seed_golden(dev, lq, lk):
     for name, t, bar in (("ctx", ctx, 2e-2), ("dq", dq, 4e-2), ("dk", dk, 4e-2), ("dv", dv, 4e-2)):
         ref = torch.from_numpy(gold["%s/%s" % (tag, name)].astype(np.float32)).to(dev)
         assert _rel(t, ref) < bar, (tag, name, _rel(t, ref))
+
+
+_FLASH_LONG_SCRIPT = r'''
+import sys, math, torch
+sys.path.insert(0, sys.argv[2])
+from k3m_amd import ops
+dev = torch.device("cuda")
+out = {}
+for (lq, lk, nh, hd, B) in ((320, 320, 4, 64, 3), (320, 36, 4, 96, 3), (37, 320, 4, 128, 2), (200, 450, 3, 128, 2),
+                            (450, 200, 2, 96, 2), (1, 300, 2, 64, 2), (300, 7, 2, 128, 2), (129, 129, 4, 64, 2),
+                            (512, 512, 2, 64, 1)):
+    D = nh * hd
+    g = torch.Generator(device="cpu").manual_seed(lq * 7 + lk)
+    q = torch.randn(B * lq, D, generator=g).to(dev).bfloat16()
+    k = torch.randn(B * lk, D, generator=g).to(dev).bfloat16()
+    v = torch.randn(B * lk, D, generator=g).to(dev).bfloat16()
+    mask = torch.zeros(B, lk, device=dev)
+    mask[:, max(1, lk - 5):] = -10000.0
+    ctx = torch.empty(B * lq, D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * nh * lq, device=dev)
+    sc = 1 / math.sqrt(hd)
+    ops.flash_attn_fwd(q, k, v, mask, ctx, lse, B, lq, lk, nh, hd, sc, 0.1, 3, 17)
+    dctx = torch.randn(B * lq, D, generator=g).to(dev).bfloat16()
+    gr = [torch.full((B * n_, D), float("nan"), device=dev, dtype=torch.bfloat16) for n_ in (lq, lk, lk)]
+    ops.flash_attn_bwd(dctx, ctx, q, k, v, mask, lse, *gr, B, lq, lk, nh, hd, sc, 0.1, 3, 17)
+    for name, t in zip(("dq", "dk", "dv", "ctx", "lse"), gr + [ctx, lse]):
+        out["%dx%dx%d_%s" % (lq, lk, hd, name)] = t.float().cpu()
+torch.cuda.synchronize()
+torch.save(out, sys.argv[1])
+'''
+
+
+def test_flash_long_bwd_dma_bit_identical_to_register_form(tmp_path):
+    """attention_flash_long.hip's LDS-DMA forward and backward (K3M_FLASH_LONG_FWD / _BWD = 2, default) against the
+    register-staged ones (= 1): same arithmetic, rows past lq / lk staged as clamped copies whose scores carry the -inf
+    mask (forward) or whose P, Pd and dS are exactly 0 (backward), so the context, the LSE, dQ, dK and dV are
+    bit-identical — config-5 shapes, multi-group heads (d = 96 / 128 past 224 keys), ragged, a single query, the 512
+    maximum, dropout on.  The knobs are read at library load: one process per setting."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "flash_long_case.py"
+    script.write_text(_FLASH_LONG_SCRIPT)
+    res = {}
+    for fwd, bwd in (("1", "1"), ("2", "1"), ("2", "2")):
+        path = str(tmp_path / ("out_%s%s.pt" % (fwd, bwd)))
+        env = dict(os.environ, K3M_FLASH_LONG_FWD=fwd, K3M_FLASH_LONG_BWD=bwd)
+        subprocess.run([sys.executable, str(script), path, repo], check=True, env=env, timeout=240)
+        res[fwd + bwd] = torch.load(path, weights_only=True)
+    bad = []
+    for x, y in (("11", "21"), ("21", "22")):   # the forward alone, then the backward alone
+        for k in res[x]:
+            a, b = res[x][k], res[y][k]
+            assert torch.isfinite(b).all(), (y, k)
+            if not torch.equal(a, b):
+                bad.append((x, y, k, float((a - b).abs().max()), int((a != b).sum()), a.numel()))
+    assert not bad, bad
