@@ -192,6 +192,7 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_fwd_kernel(con
   const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
   const int hoff = h * hd;
   const long long pbase = ((long long)s * nh + h) * lq * lk;
+  const long long rbase = ((long long)s * nh + h) * lq;   // first score row (attention dropout counters)
   ATT_STAMP(0);
 
   // additive key mask of the lane's key column in each 32-column tile (-inf on padding columns),
@@ -280,13 +281,13 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_fwd_kernel(con
         // values computed unconditionally; only the stores are predicated
         const float e0 = x0[u] * inv;
         const bool ok0 = lane < lk;
-        const float pd0 = ok0 ? e0 * k3m_drop(dr, off + prow + lane) : 0.f;
+        const float pd0 = ok0 ? e0 * k3m_attn_drop(dr, off, rbase + i, lk, lane) : 0.f;
         if (ok0) probs[prow + lane] = e0;
         if (lane < LK) Ss[sw(i, lane, LK)] = pd0;
         if (TWO) {
           const float e1 = x1[u] * inv;
           const bool ok1 = lane + 64 < lk;
-          const float pd1 = ok1 ? e1 * k3m_drop(dr, off + prow + lane + 64) : 0.f;
+          const float pd1 = ok1 ? e1 * k3m_attn_drop(dr, off, rbase + i, lk, lane + 64) : 0.f;
           if (ok1) probs[prow + lane + 64] = e1;
           if (lane + 64 < LK) Ss[sw(i, lane + 64, LK)] = pd1;
         }
@@ -347,6 +348,7 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
   const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
   const int hoff = h * hd;
   const long long pbase = ((long long)s * nh + h) * lq * lk;
+  const long long rbase = ((long long)s * nh + h) * lq;   // first score row (attention dropout counters)
   const K3mDrop dr = k3m_drop_init(seed, p_drop);
   ATT_STAMP(0);
 
@@ -395,7 +397,7 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = i0 + (r & 3) + 8 * (r >> 2) + 4 * kl;
-        const float ds = pr[r] * (acc[r] * k3m_drop(dr, off + pbase + (long long)i * lk + j) - Ds[i]);
+        const float ds = pr[r] * (acc[r] * k3m_attn_drop(dr, off, rbase + i, lk, j) - Ds[i]);
         R3[sw(i, j, LK)] = (i < lq && j < lk) ? ds : 0.f;
       }
     }
@@ -439,7 +441,7 @@ __global__ __launch_bounds__(NW * 64, ML == 64 ? 3 : 1) void attn_bwd_kernel(con
       const int e = threadIdx.x + u * NTH;
       if (e < LQ * LK) {
         const int i = e / LK, j = e - i * LK;
-        R2[sw(i, j, LK)] = pv[u] * k3m_drop(dr, off + pbase + (long long)i * lk + j);
+        R2[sw(i, j, LK)] = pv[u] * k3m_attn_drop(dr, off, rbase + i, lk, j);
       }
     }
   }
@@ -528,6 +530,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_reg_kernel(const float* __res
   const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
   const int hoff = h * HD;
   const long long pbase = ((long long)s * nh + h) * lq * lk;
+  const long long rbase = ((long long)s * nh + h) * lq;   // first score row (attention dropout counters)
   const int qi = 32 * w + cl;    // this lane's query
   ATT_STAMP(0);
 
@@ -623,6 +626,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_reg_kernel(const float* __res
     const K3mDrop dr = k3m_drop_init(seed, p_drop);
     const bool qok = qi < lq;
     const long long prow = pbase + (long long)(qok ? qi : 0) * lk;
+    const K3mPairRow prr = k3m_pair_row(dr, off, rbase + (qok ? qi : 0), lk, 4 * kl);
     const bool vec = (lk & 3) == 0;
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
@@ -630,12 +634,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_reg_kernel(const float* __res
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
           const int j0 = 32 * kt + 8 * a + 4 * kl;
+          // keys j0 .. j0 + 3: two pair draws (k3m_attn_drop); all ones when p = 0
+          const uint32_t h01 = dr.thr != 0u ? k3m_pair_draw(prr, 16 * kt + 4 * a) : 0xffffffffu;
+          const uint32_t h23 = dr.thr != 0u ? k3m_pair_draw(prr, 16 * kt + 4 * a + 1) : 0xffffffffu;
           float p4[4];
 #pragma unroll
           for (int b = 0; b < 4; ++b) {
             const int j = j0 + b;
             p4[b] = acc[kt][4 * a + b] * inv;
-            acc[kt][4 * a + b] = j < lk ? p4[b] * k3m_drop(dr, off + prow + j) : 0.f;
+            const float dm = k3m_attn_half(b < 2 ? h01 : h23, b) >= dr.thr16 ? dr.scale : 0.f;
+            acc[kt][4 * a + b] = j < lk ? p4[b] * dm : 0.f;
           }
 #ifdef K3M_LAB_NO_PSTORE   // lab only (scripts/lab/lab_build.sh): the forward without its probability stores
           if (false) {
@@ -766,6 +774,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x6_kernel(const float* __rest
   const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
   const int hoff = h * HD;
   const long long pbase = ((long long)s * nh + h) * lq * lk;
+  const long long rbase = ((long long)s * nh + h) * lq;   // first score row (attention dropout counters)
   const int qi = 32 * w + cl;
 
   // staging: K row-major (chunk-swizzled), V transposed (keys of one d contiguous), the mask
@@ -889,6 +898,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x6_kernel(const float* __rest
     const K3mDrop dr = k3m_drop_init(seed, p_drop);
     const bool qok = qi < lq;
     const long long prow = pbase + (long long)(qok ? qi : 0) * lk;
+    const K3mPairRow prr = k3m_pair_row(dr, off, rbase + (qok ? qi : 0), lk, 4 * kl);
     const bool vec = (lk & 3) == 0;
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
@@ -896,12 +906,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x6_kernel(const float* __rest
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
           const int j0 = 32 * kt + 8 * a + 4 * kl;
+          // keys j0 .. j0 + 3: two pair draws (k3m_attn_drop); all ones when p = 0
+          const uint32_t h01 = dr.thr != 0u ? k3m_pair_draw(prr, 16 * kt + 4 * a) : 0xffffffffu;
+          const uint32_t h23 = dr.thr != 0u ? k3m_pair_draw(prr, 16 * kt + 4 * a + 1) : 0xffffffffu;
           float p4[4];
 #pragma unroll
           for (int b = 0; b < 4; ++b) {
             const int j = j0 + b;
             p4[b] = acc[kt][4 * a + b] * inv;
-            acc[kt][4 * a + b] = j < lk ? p4[b] * k3m_drop(dr, off + prow + j) : 0.f;
+            const float dm = k3m_attn_half(b < 2 ? h01 : h23, b) >= dr.thr16 ? dr.scale : 0.f;
+            acc[kt][4 * a + b] = j < lk ? p4[b] * dm : 0.f;
           }
 #ifdef K3M_LAB_NO_PSTORE   // lab only (scripts/lab/lab_build.sh): the forward without its probability stores
           if (false) {
@@ -1011,6 +1025,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_reg_kernel(
   const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
   const int hoff = h * HD;
   const long long pbase = ((long long)s * nh + h) * lq * lk;
+  const long long rbase = ((long long)s * nh + h) * lq;   // first score row (attention dropout counters)
   const K3mDrop dr = k3m_drop_init(seed, p_drop);
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   ATT_STAMP(0);
@@ -1121,7 +1136,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_reg_kernel(
           for (int b = 0; b < 4; ++b) {
             const int r = 4 * a + b, qr = 32 * qt + 8 * a + 4 * kl + b;
             const bool ok = qr < lq && key < lk;
-            const float m = k3m_drop(dr, off + pbase + (long long)(ok ? qr : 0) * lk + (ok ? key : 0));
+            const float m = k3m_attn_drop(dr, off, rbase + (ok ? qr : 0), lk, ok ? key : 0);
             const float p = pdv[qt][r];
             acc[qt][r] = ok ? p * (acc[qt][r] * m - dd[b]) : 0.f;
             pdv[qt][r] = p * m;
@@ -1323,6 +1338,7 @@ __global__ __launch_bounds__(ML * 2, 1) void attn_bwd_x6km_kernel(
   const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
   const int hoff = h * HD;
   const long long pbase = ((long long)s * nh + h) * lq * lk;
+  const long long rbase = ((long long)s * nh + h) * lq;   // first score row (attention dropout counters)
   const K3mDrop dr = k3m_drop_init(seed, p_drop);
   const int NQT = LQ >> 5;
   const int j = 32 * w + cl;     // this lane's key in the key phase
@@ -1420,6 +1436,8 @@ __global__ __launch_bounds__(ML * 2, 1) void attn_bwd_x6km_kernel(
       for (int ks = 0; ks < KS; ++ks)
         x6_mma(dP, k6_row<NC>(dOs, 32 * it, ks, lane), k6_row<NC>(dOs + PQ, 32 * it, ks, lane),
                k6_row<NC>(dOs + 2 * PQ, 32 * it, ks, lane), vh[ks], vm[ks], vl[ks]);
+      // keep bits of this lane's key for the tile's 16 rows (padding rows / keys: P = 0 above)
+      const uint32_t keep = dr.thr != 0u ? k3m_attn_keep_km16(dr, off, rbase + 32 * it, 4 * kl, lk, j) : 0xffffu;
       floatx16 Pd;
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
@@ -1428,8 +1446,8 @@ __global__ __launch_bounds__(ML * 2, 1) void attn_bwd_x6km_kernel(
         const float dd[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-          const int r = 4 * a + b, i = i0 + b;
-          const float m = k3m_drop(dr, off + pbase + (long long)min(i, lq - 1) * lk + jc);
+          const int r = 4 * a + b;
+          const float m = k3m_keep_f(keep, r, __float_as_uint(dr.scale));
           Pd[r] = p[r] * m;
           dP[r] = p[r] * (dP[r] * m - dd[b]);   // dS
         }

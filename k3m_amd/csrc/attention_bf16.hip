@@ -165,18 +165,37 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __rest
   const float inv = 1.f / sum;
   const long long prow = ((long long)s * nh + h) * lq + i;   // row of the [nseq, nh, lq] LSE
   if (kl == 0 && i < lq) lse[prow] = mx + __logf(sum);
-  const long long pbase = prow * lk;
+  if (p_drop > 0.f) {
+    // registers 4 q + b of tile jt are keys 32 jt + 8 q + 4 kl + b: pairs (b = 0, 1), (2, 3) share one draw, pair
+    // counter pb + 16 jt + 4 q + b / 2 (k3m_attn_drop), the high word mixed once (and once more for a carry)
+    const K3mDrop dr = k3m_drop_init(seed, p_drop);
+    const uint64_t pb = off + (uint64_t)prow * (uint64_t)((lk + 1) >> 1) + (uint64_t)(2 * kl);
+    const uint32_t lo = (uint32_t)pb, pre0 = k3m_pair_pre(dr.key, pb), pre1 = k3m_pair_pre(dr.key, pb + (1ull << 32));
 #pragma unroll
-  for (int jt = 0; jt < MAXL / 32; ++jt)
-    if (jt < NJT) {
+    for (int jt = 0; jt < MAXL / 32; ++jt)
+      if (jt < NJT) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int j = 32 * jt + (r & 3) + 8 * (r >> 2) + 4 * kl;
-        float pv = S[jt][r] * inv;
-        if (p_drop > 0.f) pv *= (i < lq && j < lk) ? k3m_dropout_scale(seed, off + pbase + j, p_drop) : 0.f;
-        S[jt][r] = pv;
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int hb = 0; hb < 2; ++hb) {
+            const uint32_t x = lo + (uint32_t)(16 * jt + 4 * q + hb);
+            const uint32_t hh = k3m_mix32(x ^ (x < lo ? pre1 : pre0));
+#pragma unroll
+            for (int b2 = 0; b2 < 2; ++b2) {
+              const int r = 4 * q + 2 * hb + b2, j = 32 * jt + 8 * q + 4 * kl + 2 * hb + b2;
+              const bool kept = i < lq && j < lk && k3m_attn_half(hh, b2) >= dr.thr16;
+              S[jt][r] = kept ? S[jt][r] * inv * dr.scale : 0.f;
+            }
+          }
       }
-    }
+  } else {
+#pragma unroll
+    for (int jt = 0; jt < MAXL / 32; ++jt)
+      if (jt < NJT) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) S[jt][r] *= inv;
+      }
+  }
   // O = P V
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) {
@@ -274,7 +293,6 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kernel(const uint16_t* __rest
     const int i = i0 + cl;
     const float li = Ls[i], di = Ds[i];
     const bool iv = i < lq;
-    const long long pbase = (lrow0 + i) * lk;
     floatx16 dQ[DT];
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) dQ[dt] = zero16();
@@ -294,7 +312,7 @@ __global__ __launch_bounds__(NT, 1) void flash_bwd_kernel(const uint16_t* __rest
       for (int r = 0; r < 16; ++r) {
         const int j = 32 * jt + (r & 3) + 8 * (r >> 2) + 4 * kl;
         const float p = iv ? __expf(St[r] * scale + msk[j] - li) : 0.f;
-        const float dm = (p_drop > 0.f && iv && j < lk) ? k3m_dropout_scale(seed, off + pbase + j, p_drop) : 1.f;
+        const float dm = (p_drop > 0.f && iv && j < lk) ? k3m_attn_dropout_scale(seed, p_drop, off, lrow0 + i, lk, j) : 1.f;
         pd[r] = p * dm;
         ds[r] = p * (dP[r] * dm - di);
       }
@@ -511,6 +529,9 @@ __global__ __launch_bounds__(NW * 64, km_occupancy<HD>()) void flash_bwd_km_kern
 #pragma unroll
     for (int it = 0; it < MAXL / 32; ++it) {
       if (it >= NQT) break;
+      // dropout keep bits of this lane's key for the tile's 16 query rows (register r), drawn before the products;
+      // padding rows and keys draw unused values (P = 0 there)
+      const uint32_t keep = dr.thr != 0u ? k3m_attn_keep_km16(dr, off, lrow0 + 32 * it, 4 * kl, lk, j) : 0xffffu;
       floatx16 S = zero16(), dP = zero16();
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -526,9 +547,9 @@ __global__ __launch_bounds__(NW * 64, km_occupancy<HD>()) void flash_bwd_km_kern
         const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-          const int r = 4 * a + b, i = i0 + b;
+          const int r = 4 * a + b;
           const float p = __expf(S[r] * scale + mj - lv[b]);
-          const float dm = k3m_drop(dr, off + (lrow0 + min(i, lq - 1)) * lk + min(j, lk - 1));
+          const float dm = k3m_keep_f(keep, r, __float_as_uint(dr.scale));
           S[r] = p * dm;                          // P_drop
           dP[r] = p * (dP[r] * dm - dv4[b]);      // dS
         }

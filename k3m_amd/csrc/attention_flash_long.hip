@@ -150,16 +150,14 @@ __global__ __launch_bounds__(FNT, 2) void flash_long_fwd_kernel(const uint16_t* 
       m2 = mn;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
-      // dropout counter off + prow lk + j = cb + a compile-time offset per register (64-bit math once per chunk);
       // keys past lk draw an unused value (p = 0 there)
-      const uint64_t cb = off + (uint64_t)prow * (uint64_t)lk + (uint64_t)(c * FKC + 4 * kl);
 #pragma unroll
       for (int jt = 0; jt < FKC / 32; ++jt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float p = __builtin_amdgcn_exp2f(S[jt][r] - mref);
           lp = jt == 0 && r == 0 ? fmaf(lp, alpha, p) : lp + p;   // the rescale fused explicitly (fwd2 does the same)
-          S[jt][r] = p * k3m_drop(dr, cb + (uint64_t)(32 * jt + (r & 3) + 8 * (r >> 2)));
+          S[jt][r] = p * k3m_attn_drop(dr, off, prow, lk, c * FKC + 32 * jt + (r & 3) + 8 * (r >> 2) + 4 * kl);
         }
       // O^T += V^T P^T: A = V image read transposed in the accumulator k order, B = P from the registers
 #pragma unroll
@@ -337,16 +335,9 @@ __global__ __launch_bounds__(bwd_max_waves<HD>() * 64, 1) void flash_long_bwd_ke
     // ---- key phase
     if (kw) {
       // this lane's dropout keep bits for the chunk (register r = 4 a + b <-> query q0 + 8 a + 4 kl + b), drawn
-      // before the products so the hash temporaries are not live beside the S / dP accumulators.  Counter
-      // off + (lrow0 + i) lk + j = cb + (8 a + b) lk; query rows past lq draw unused values (p = 0 there)
-      uint32_t keep = 0xffffu;
-      if (dr.thr != 0u) {
-        const uint64_t cb = off + (uint64_t)(lrow0 + q0 + 4 * kl) * (uint64_t)lk + (uint64_t)j;
-        keep = 0u;
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          keep |= (uint32_t)((k3m_hash_key(dr.key, cb + (uint64_t)((8 * (r >> 2) + (r & 3)) * lk)) >> 8) >= dr.thr) << r;
-      }
+      // before the products so the hash temporaries are not live beside the S / dP accumulators; query rows past lq
+      // and keys past lk draw unused values (p = 0 there)
+      const uint32_t keep = dr.thr != 0u ? k3m_attn_keep_km16(dr, off, lrow0 + q0, 4 * kl, lk, j) : 0xffffu;
       floatx16 S = zero16(), dP = zero16();
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -366,7 +357,7 @@ __global__ __launch_bounds__(bwd_max_waves<HD>() * 64, 1) void flash_long_bwd_ke
         for (int b = 0; b < 4; ++b) {
           const int r = 4 * a + b;
           const float p = __builtin_amdgcn_exp2f(fmaf(S[r], sl2, mj2) - lvv[b]);
-          const float dm = (keep >> r) & 1u ? dr.scale : 0.f;
+          const float dm = k3m_keep_f(keep, r, __float_as_uint(dr.scale));
           S[r] = p * dm;                         // P_drop
           dP[r] = p * (dP[r] * dm - dvv[b]);     // dS
         }
@@ -516,6 +507,8 @@ __device__ __forceinline__ void dma_rows(uint16_t* img, int r0, const uint16_t* 
                : "memory");
 }
 
+__device__ float k3m_inf_word = INFINITY;   // LDS-DMA source of the padding rows' LSE
+
 template <int HD>
 __global__ __launch_bounds__(bwd_max_waves<HD>() * 64, 1) void flash_long_bwd2_kernel(
     const uint16_t* __restrict__ dctx, long long ldc, const uint16_t* __restrict__ q, long long ldq,
@@ -564,9 +557,9 @@ __global__ __launch_bounds__(bwd_max_waves<HD>() * 64, 1) void flash_long_bwd2_k
     for (int i = w; i < NCI; i += nw) {
       if (i < NQI) dma_rows<NC, NCL>(sl, i * RPI, q, ldq, qrow0 + q0, lq - q0, hoff, lane);
       else if (i < 2 * NQI) dma_rows<NC, NCL>(sl + BQC * HW, (i - NQI) * RPI, dctx, ldc, qrow0 + q0, lq - q0, hoff, lane);
-      else {   // raw LSE (lanes 0-31) and D (lanes 32-63) of the chunk's rows, clamped
+      else {   // raw LSE (lanes 0-31; +inf for rows past lq, so P = 0 there) and D (lanes 32-63) of the chunk's rows
         const long long lr = lrow0 + min(q0 + cl, lq - 1);
-        lds_dma4(kl ? dvec + lr : lse + lr, sl + 2 * BQC * HW);
+        lds_dma4(kl ? dvec + lr : (q0 + cl < lq ? lse + lr : &k3m_inf_word), sl + 2 * BQC * HW);
       }
     }
   };
@@ -602,14 +595,7 @@ __global__ __launch_bounds__(bwd_max_waves<HD>() * 64, 1) void flash_long_bwd2_k
     const float* Dc = Lc + BQC;
     // ---- key phase (as flash_long_bwd_kernel; LSE scaled and padding rows set to +inf here)
     if (kw) {
-      uint32_t keep = 0xffffu;
-      if (dr.thr != 0u) {
-        const uint64_t cb = off + (uint64_t)(lrow0 + q0 + 4 * kl) * (uint64_t)lk + (uint64_t)j;
-        keep = 0u;
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          keep |= (uint32_t)((k3m_hash_key(dr.key, cb + (uint64_t)((8 * (r >> 2) + (r & 3)) * lk)) >> 8) >= dr.thr) << r;
-      }
+      const uint32_t keep = dr.thr != 0u ? k3m_attn_keep_km16(dr, off, lrow0 + q0, 4 * kl, lk, j) : 0xffffu;
       floatx16 S = zero16(), dP = zero16();
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -627,9 +613,13 @@ __global__ __launch_bounds__(bwd_max_waves<HD>() * 64, 1) void flash_long_bwd2_k
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           const int r = 4 * a + b;
-          const float lvb = q0 + i0 + b < lq ? lraw[b] * LOG2E : INFINITY;   // padding query rows: P = 0
+          float lvb;   // padding query rows: +inf (the DMA above), P = 0
+          {
+#pragma clang fp contract(off)
+            lvb = lraw[b] * LOG2E;   // rounded on its own, as the register form's pre-scaled LDS copy
+          }
           const float p = __builtin_amdgcn_exp2f(fmaf(S[r], sl2, mj2) - lvb);
-          const float dm = (keep >> r) & 1u ? dr.scale : 0.f;
+          const float dm = k3m_keep_f(keep, r, __float_as_uint(dr.scale));
           S[r] = p * dm;
           dP[r] = p * (dP[r] * dm - dvv[b]);
         }
@@ -820,18 +810,29 @@ __global__ __launch_bounds__(FNT, fwd2_occ<HD>()) void flash_long_fwd2_kernel(
       m2 = mn;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
-      const uint64_t cb = off + (uint64_t)prow * (uint64_t)lk + (uint64_t)(c * FKC + 4 * kl);
-      // the p = 0 test hoisted out of the element loop (k3m_drop's per-element branch): same values
+      // the p = 0 test hoisted out of the element loop.  Registers 4 q + b of tile jt are keys
+      // c FKC + 32 jt + 8 q + 4 kl + b: pairs (b = 0, 1) and (2, 3) of one draw each, pair counters
+      // pb + 16 jt + 4 q + b / 2 from this lane's first pair pb; the high word is mixed once per chunk, for pb's high
+      // word and for the next one (a pair whose low word carried)
       if (dr.thr != 0u) {
+        const uint64_t pb = off + (uint64_t)prow * (uint64_t)((lk + 1) >> 1) + (uint64_t)(c * (FKC / 2) + 2 * kl);
+        const uint32_t lo = (uint32_t)pb, pre0 = k3m_pair_pre(dr.key, pb), pre1 = k3m_pair_pre(dr.key, pb + (1ull << 32));
 #pragma unroll
         for (int jt = 0; jt < FKC / 32; ++jt)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float p = __builtin_amdgcn_exp2f(S[jt][r] - mref);
-            lp = jt == 0 && r == 0 ? fmaf(lp, alpha, p) : lp + p;
-            const uint32_t hh = k3m_hash_key(dr.key, cb + (uint64_t)(32 * jt + (r & 3) + 8 * (r >> 2)));
-            S[jt][r] = p * ((hh >> 8) >= dr.thr ? dr.scale : 0.f);
-          }
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int hb = 0; hb < 2; ++hb) {
+              const uint32_t x = lo + (uint32_t)(16 * jt + 4 * q + hb);
+              const uint32_t hh = k3m_mix32(x ^ (x < lo ? pre1 : pre0));
+#pragma unroll
+              for (int b2 = 0; b2 < 2; ++b2) {
+                const int r = 4 * q + 2 * hb + b2;
+                const float p = __builtin_amdgcn_exp2f(S[jt][r] - mref);
+                lp = jt == 0 && r == 0 ? fmaf(lp, alpha, p) : lp + p;
+                S[jt][r] = p * (k3m_attn_half(hh, b2) >= dr.thr16 ? dr.scale : 0.f);
+              }
+            }
       } else {
 #pragma unroll
         for (int jt = 0; jt < FKC / 32; ++jt)
@@ -917,9 +918,13 @@ size_t fwd2_lds(int lk, int hd) {
 const int kFlashLongFwd = k3m_env_int("K3M_FLASH_LONG_FWD", 2);
 
 // key tiles per group and groups of a head's backward
+// K3M_FLASH_LONG_TPG (lab A/B): at most this many 32-key tiles per backward workgroup (0: as many as fit)
+const int kFlashLongTpg = k3m_env_int("K3M_FLASH_LONG_TPG", 0);
+
 void bwd_groups(int lk, int hd, int& tpg, int& ngrp, int& nw) {
   const int nkt = (lk + 31) / 32;
-  const int cap = hd == 64 ? bwd_max_waves<64>() : bwd_max_waves<128>();
+  int cap = hd == 64 ? bwd_max_waves<64>() : bwd_max_waves<128>();
+  if (kFlashLongTpg > 0) cap = std::min(cap, kFlashLongTpg);
   ngrp = (nkt + cap - 1) / cap;
   tpg = (nkt + ngrp - 1) / ngrp;
   nw = std::max(tpg, BMIN_W);

@@ -72,6 +72,7 @@ __global__ __launch_bounds__(NT) void long_fwd_kernel(const T* __restrict__ q, l
   const long long qrow0 = (long long)s * lq + i0, krow0 = (long long)s * lk;
   const int hoff = h * hd, nq = min(QB, lq - i0);
   const long long pbase = ((long long)s * nh + h) * lq * lk;
+  const long long rbase = ((long long)s * nh + h) * lq;   // first score row (attention dropout counters)
   stage<T>(Qs, q, qrow0, ldq, hoff, QB, nq, hd);
   for (int c0 = 0; c0 < LKP; c0 += CH) {
     __syncthreads();
@@ -120,7 +121,7 @@ __global__ __launch_bounds__(NT) void long_fwd_kernel(const T* __restrict__ q, l
         if (act && j < lk) {
           const float p = x[u] * inv;
           probs[prow + j] = p;
-          pd = p * k3m_dropout_scale(seed, off + prow + j, p_drop);
+          pd = p * k3m_attn_dropout_scale(seed, p_drop, off, rbase + i0 + i, lk, j);
         }
         Ss[sw(i, j, LKP)] = pd;
       }
@@ -167,6 +168,7 @@ __global__ __launch_bounds__(NT) void long_bwd_q_kernel(const T* __restrict__ dc
   const long long qrow0 = (long long)s * lq + i0, krow0 = (long long)s * lk;
   const int hoff = h * hd, nq = min(QB, lq - i0);
   const long long pbase = ((long long)s * nh + h) * lq * lk;
+  const long long rbase = ((long long)s * nh + h) * lq;   // first score row (attention dropout counters)
   stage<T>(R1, dctx, qrow0, ldc, hoff, QB, nq, hd);
   for (int i = w; i < QB; i += NW) {   // D_i = dO_i . O_i
     float a = 0.f;
@@ -192,7 +194,7 @@ __global__ __launch_bounds__(NT) void long_bwd_q_kernel(const T* __restrict__ dc
       float ds = 0.f;
       if (i < nq && j < lk) {
         const long long pidx = pbase + (long long)(i0 + i) * lk + j;
-        ds = probs[pidx] * (acc[r] * k3m_dropout_scale(seed, off + pidx, p_drop) - Ds[i]);
+        ds = probs[pidx] * (acc[r] * k3m_attn_dropout_scale(seed, p_drop, off, rbase + i0 + i, lk, j) - Ds[i]);
         ds_ws[pidx] = ds;
       }
       Ss[sw(i, j, LKP)] = ds;
@@ -238,6 +240,7 @@ __global__ __launch_bounds__(NT) void long_bwd_kv_kernel(const T* __restrict__ d
   const long long qrow = (long long)s * lq, krow0 = (long long)s * lk + j0b;
   const int hoff = h * hd, nk = min(KB, lk - j0b);
   const long long pbase = ((long long)s * nh + h) * lq * lk;
+  const long long rbase = ((long long)s * nh + h) * lq;   // first score row (attention dropout counters)
   const int ntile = (KB / 32) * (hd / 32);   // <= 8: at most two per wave
   for (int pass = 0; pass < 2; ++pass) {     // 0: dV = Pd^T dO   1: dK = scale dS^T Q
     floatx16 acc[2];
@@ -254,7 +257,7 @@ __global__ __launch_bounds__(NT) void long_bwd_kv_kernel(const T* __restrict__ d
         float x = 0.f;
         if (i < nrow && j < nk) {
           const long long pidx = pbase + (long long)(c0 + i) * lk + j0b + j;
-          x = pass == 0 ? probs[pidx] * k3m_dropout_scale(seed, off + pidx, p_drop) : ds_ws[pidx];
+          x = pass == 0 ? probs[pidx] * k3m_attn_dropout_scale(seed, p_drop, off, rbase + c0 + i, lk, j0b + j) : ds_ws[pidx];
         }
         Ps[sw(i, j, KB)] = x;
       }

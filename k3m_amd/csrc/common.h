@@ -79,13 +79,15 @@ __device__ __forceinline__ uint32_t k3m_hash(uint64_t seed, uint64_t ctr) {
 // so the test is one integer compare.  Set up once per launch (wave-uniform) with k3m_drop_init.
 struct K3mDrop {
   uint64_t key;
-  uint32_t thr;   // 0: p == 0, nothing dropped
+  uint32_t thr;     // 0: p == 0, nothing dropped
+  uint32_t thr16;   // ceil(p * 2^16): the attention draws' 16-bit threshold
   float scale;
 };
 __device__ __forceinline__ K3mDrop k3m_drop_init(uint64_t seed, float p) {
   K3mDrop d;
   d.key = k3m_seed_key(seed);
   d.thr = p > 0.f ? (uint32_t)ceilf(p * 16777216.0f) : 0u;
+  d.thr16 = p > 0.f ? (uint32_t)ceilf(p * 65536.0f) : 0u;
   d.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   return d;
 }
@@ -95,6 +97,73 @@ __device__ __forceinline__ float k3m_drop(const K3mDrop& d, uint64_t ctr) {
 }
 __device__ __forceinline__ float k3m_dropout_scale(uint64_t seed, uint64_t ctr, float p) {
   return k3m_drop(k3m_drop_init(seed, p), ctr);
+}
+// Attention-probability dropout: one 32-bit draw per PAIR of keys.  Element (row, j) of a score block with lk keys
+// per row (row = (sequence * heads + head) * lq + query) takes the (j & 1) half of
+//   k3m_hash_key(key, off + row * ceil(lk / 2) + j / 2)
+// and is kept iff that 16-bit value >= thr16 = ceil(p * 2^16).  The softmax of every attention kernel is VALU-bound
+// and the hash was the largest part of it (three 32-bit multiplies per score): this halves the hashing, and a lane
+// that holds both keys of a pair (the flash forwards) or swaps bits with the lane that does (the key-major
+// backwards) draws once for two scores.  p resolves to 2^-16.
+__device__ __forceinline__ uint64_t k3m_attn_ctr(uint64_t off, long long row, int lk, int j) {
+  return off + (uint64_t)row * (uint64_t)((lk + 1) >> 1) + (uint64_t)(j >> 1);
+}
+__device__ __forceinline__ uint32_t k3m_attn_half(uint32_t h, int j) { return (j & 1) ? h >> 16 : h & 0xffffu; }
+__device__ __forceinline__ float k3m_attn_drop(const K3mDrop& d, uint64_t off, long long row, int lk, int j) {
+  if (d.thr == 0u) return 1.f;
+  return k3m_attn_half(k3m_hash_key(d.key, k3m_attn_ctr(off, row, lk, j)), j) >= d.thr16 ? d.scale : 0.f;
+}
+__device__ __forceinline__ float k3m_attn_dropout_scale(uint64_t seed, float p, uint64_t off, long long row, int lk,
+                                                       int j) {
+  return k3m_attn_drop(k3m_drop_init(seed, p), off, row, lk, j);
+}
+// The high-word half of k3m_hash_key for counters that share ctr's high word: for a lane's run of pairs
+// ctr + d whose low word does not carry (the caller checks),
+//   k3m_hash_key(key, ctr + d) == k3m_mix32(((uint32_t)ctr + d) ^ k3m_pair_pre(key, ctr)).
+__device__ __forceinline__ uint32_t k3m_pair_pre(uint64_t key, uint64_t ctr) {
+  return (uint32_t)key ^ (((uint32_t)(ctr >> 32) ^ (uint32_t)(key >> 32)) * 0x9E3779B1u);
+}
+// dropout factor of bit r of a keep mask: scale (its bits sbits) or +0 -- a sign-extended bit field and an AND
+__device__ __forceinline__ float k3m_keep_f(uint32_t keep, int r, uint32_t sbits) {
+  return __uint_as_float((uint32_t)((int)(keep << (31 - r)) >> 31) & sbits);
+}
+// A row's pair draws from a lane's first pair (key jb, even): k3m_pair_draw(pr, d) is the draw of keys jb + 2 d and
+// jb + 2 d + 1 (k3m_attn_drop), the high word mixed once per row and once more for a low word that carries.
+struct K3mPairRow {
+  uint32_t lo, pre0, pre1;
+};
+__device__ __forceinline__ K3mPairRow k3m_pair_row(const K3mDrop& d, uint64_t off, long long row, int lk, int jb) {
+  const uint64_t pb = k3m_attn_ctr(off, row, lk, jb);
+  return {(uint32_t)pb, k3m_pair_pre(d.key, pb), k3m_pair_pre(d.key, pb + (1ull << 32))};
+}
+__device__ __forceinline__ uint32_t k3m_pair_draw(const K3mPairRow& pr, uint32_t d) {
+  const uint32_t x = pr.lo + d;
+  return k3m_mix32(x ^ (x < pr.lo ? pr.pre1 : pr.pre0));
+}
+// Keep bits of a key-major lane (the backward kernels: this lane's key j, query rows rowu + rowl + 8 (r >> 2) +
+// (r & 3) in bit r = 0 .. 15, the MFMA 32x32 accumulator order; rowu wave-uniform, rowl the lane's small part).
+// Lanes 2m and 2m + 1 hold the keys of one pair for the same rows: the even lane draws the pair's values of rows
+// r < 8, the odd lane those of r >= 8, and each passes the other key's 8 bits across with one DPP lane swap -- 8
+// draws per lane instead of 16.  Needs j's parity == the lane's and both lanes of the pair active (key-major
+// kernels index keys by lane from an even base, under wave-uniform branches).
+__device__ __forceinline__ uint32_t k3m_attn_keep_km16(const K3mDrop& d, uint64_t off, long long rowu, int rowl, int lk,
+                                                       int j) {
+  const int odd = j & 1;
+  const uint32_t lkp = (uint32_t)((lk + 1) >> 1);
+  const uint64_t ub = off + (uint64_t)rowu * lkp;                           // wave-uniform
+  uint32_t rel = (uint32_t)(rowl + 16 * odd) * lkp + (uint32_t)(j >> 1);   // < 2^32: rows and keys <= 512
+  // opaque to loop-invariant code motion: the callers draw once per query chunk, and the eight per-row counters
+  // hoisted out of that loop held 8 - 16 VGPRs across it (the d = 64 backward spilled)
+  asm volatile("" : "+v"(rel));
+  uint32_t mine = 0u, theirs = 0u;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const uint32_t h = k3m_hash_key(d.key, ub + (uint64_t)(rel + (uint32_t)(8 * (t >> 2) + (t & 3)) * lkp));
+    mine |= (uint32_t)(k3m_attn_half(h, odd) >= d.thr16) << t;
+    theirs |= (uint32_t)(k3m_attn_half(h, odd ^ 1) >= d.thr16) << t;
+  }
+  const uint32_t got = (uint32_t)__builtin_amdgcn_mov_dpp((int)theirs, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
+  return odd ? (got | (mine << 8)) : (mine | (got << 8));
 }
 // uniform in the OPEN interval (0, 1): both log(u) and log(-log(u)) stay finite (gumbel noise)
 __device__ __forceinline__ float k3m_uniform(uint64_t seed, uint64_t ctr) {

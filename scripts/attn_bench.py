@@ -10,6 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from k3m_amd import ops, _lib as L  # noqa: E402
 
 B = 64
+P_DROP = float(os.environ.get("ATTN_P", "0.1"))   # attention-probability dropout of the timed calls
 SHAPES = [  # name, nseq, lq, lk, nh, hd
     ("text T", 2 * B, 36, 36, 12, 64),
     ("text P", 2 * B, 128, 128, 12, 64),
@@ -51,15 +52,15 @@ def run(name, nseq, lq, lk, nh, hd, dtype, reps=20):
 
     def fwd():
         if flash:
-            ops.flash_attn_fwd(q, k, v, mask, ctx, lse, nseq, lq, lk, nh, hd, sc, 0.1, 7, 0)
+            ops.flash_attn_fwd(q, k, v, mask, ctx, lse, nseq, lq, lk, nh, hd, sc, P_DROP, 7, 0)
         else:
-            ops.attn_fwd(q, k, v, mask, ctx, probs, nseq, lq, lk, nh, hd, sc, 0.1, 7, 0)
+            ops.attn_fwd(q, k, v, mask, ctx, probs, nseq, lq, lk, nh, hd, sc, P_DROP, 7, 0)
 
     def bwd():
         if flash:
-            ops.flash_attn_bwd(dctx, ctx, q, k, v, mask, lse, dq, dk, dv, nseq, lq, lk, nh, hd, sc, 0.1, 7, 0)
+            ops.flash_attn_bwd(dctx, ctx, q, k, v, mask, lse, dq, dk, dv, nseq, lq, lk, nh, hd, sc, P_DROP, 7, 0)
         else:
-            ops.attn_bwd(dctx, ctx, q, k, v, probs, dq, dk, dv, nseq, lq, lk, nh, hd, sc, 0.1, 7, 0)
+            ops.attn_bwd(dctx, ctx, q, k, v, probs, dq, dk, dv, nseq, lq, lk, nh, hd, sc, P_DROP, 7, 0)
     res = []
     for f in (fwd, bwd):
         for _ in range(3):

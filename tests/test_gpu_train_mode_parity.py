@@ -90,7 +90,7 @@ def test_bert_layer_train_mode(eng, kind):
     torch.cuda.synchronize()
     # the layer's counters: attention probabilities, then the two residual tails (Rng.take order)
     na, nh_ = nseq * nh * L * L, nseq * L * H
-    drop = {"attn": torch.from_numpy(DM.keep_scale(rng.seed, 0, na, pa)),
+    drop = {"attn": torch.from_numpy(DM.attn_keep_scale(rng.seed, 0, nseq * nh * L, L, pa)),
             "attn_out": torch.from_numpy(DM.keep_scale(rng.seed, na, nh_, ph)),
             "ffn_out": torch.from_numpy(DM.keep_scale(rng.seed, na + nh_, nh_, ph))}
     P = _p64(eng, pre)
@@ -160,9 +160,14 @@ def test_coattention_layer_train_mode(eng, kind, lockstep):
     n12 = nseq * nb * L1 * L2
     sizes = dict(attn1=n12, attn2=n12, out1=nseq * L1 * H1, out2=nseq * L2 * H2, ffn1=nseq * L1 * H1,
                  ffn2=nseq * L2 * H2)
+    # attention score blocks: probs1 = stream-2 queries (L2) over stream-1 keys (L1), probs2 the reverse
+    attn_rows = dict(attn1=(nseq * nb * L2, L1), attn2=(nseq * nb * L1, L2))
     drop, off = {}, 0
     for site, p in _co_rates(c, kind):
-        drop[site] = torch.from_numpy(DM.keep_scale(rng.seed, off, sizes[site], p))
+        if site in attn_rows:
+            drop[site] = torch.from_numpy(DM.attn_keep_scale(rng.seed, off, *attn_rows[site], p))
+        else:
+            drop[site] = torch.from_numpy(DM.keep_scale(rng.seed, off, sizes[site], p))
         off += sizes[site]
     P = _p64(eng, pre)
     r1 = s1.double().view(nseq, L1, H1).requires_grad_(True)
