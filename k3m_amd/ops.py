@@ -288,7 +288,7 @@ def small_splitk(m, n, k):
     """k-split of a small fp32 product (few 64 x 64 tiles, long k: the m = 64 pooled / gate projections, the
     389-row region-head GEMMs): one workgroup per (tile, k-slice) instead of one per tile walking all of k, the
     requested epilogue applied by the split-K reduction.  1 = no split."""
-    if not SMALL_SPLITK:
+    if not SMALL_SPLITK or m <= 0 or n <= 0 or k <= 0:   # empty products (e.g. a batch with no labelled rows)
         return 1
     if n <= 8:
         # the skinny kernel (gemm.hip gemm_skinny_kernel, 64 rows per workgroup): k-slices of >= 128 until the
