@@ -509,7 +509,7 @@ __device__ __forceinline__ void dma_rows(uint16_t* img, int r0, const uint16_t* 
 
 __device__ float k3m_inf_word = INFINITY;   // LDS-DMA source of the padding rows' LSE
 
-template <int HD>
+template <int HD, bool DQ2>
 __global__ __launch_bounds__(bwd_max_waves<HD>() * 64, 1) void flash_long_bwd2_kernel(
     const uint16_t* __restrict__ dctx, long long ldc, const uint16_t* __restrict__ q, long long ldq,
     const uint16_t* __restrict__ k, long long ldk, const uint16_t* __restrict__ v, long long ldv,
@@ -530,7 +530,7 @@ __global__ __launch_bounds__(bwd_max_waves<HD>() * 64, 1) void flash_long_bwd2_k
   uint16_t* Kimg = smem;                       // [GK][HW]
   uint16_t* Vimg = Kimg + GK * HW;             // [GK][HW]
   uint16_t* dSt = Vimg + GK * HW;              // [GK][BQC]
-  uint16_t* ring = dSt + GK * BQC;             // nqb x {Q [BQC][HW], dO [BQC][HW], LSE [32] f32, D [32] f32}
+  uint16_t* ring = dSt + (DQ2 ? 2 : 1) * GK * BQC;   // nqb x {Q [BQC][HW], dO [BQC][HW], LSE [32] f32, D [32] f32}
   const int s = blockIdx.x / nh, h = blockIdx.x % nh, grp = blockIdx.y, ngrp = gridDim.y;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
@@ -554,12 +554,17 @@ __global__ __launch_bounds__(bwd_max_waves<HD>() * 64, 1) void flash_long_bwd2_k
   auto dma_chunk = [&](int c) {
     uint16_t* sl = ring + (c % nqb) * SL;
     const int q0 = c * BQC;
+    // the lane index made opaque here: per-lane offsets hoisted out of the chunk loop spilled at d = 64, and the
+    // reload's vmcnt(0) drained the DMA ring at every chunk
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
     for (int i = w; i < NCI; i += nw) {
-      if (i < NQI) dma_rows<NC, NCL>(sl, i * RPI, q, ldq, qrow0 + q0, lq - q0, hoff, lane);
-      else if (i < 2 * NQI) dma_rows<NC, NCL>(sl + BQC * HW, (i - NQI) * RPI, dctx, ldc, qrow0 + q0, lq - q0, hoff, lane);
+      if (i < NQI) dma_rows<NC, NCL>(sl, i * RPI, q, ldq, qrow0 + q0, lq - q0, hoff, ln);
+      else if (i < 2 * NQI) dma_rows<NC, NCL>(sl + BQC * HW, (i - NQI) * RPI, dctx, ldc, qrow0 + q0, lq - q0, hoff, ln);
       else {   // raw LSE (lanes 0-31; +inf for rows past lq, so P = 0 there) and D (lanes 32-63) of the chunk's rows
-        const long long lr = lrow0 + min(q0 + cl, lq - 1);
-        lds_dma4(kl ? dvec + lr : (q0 + cl < lq ? lse + lr : &k3m_inf_word), sl + 2 * BQC * HW);
+        const int kh = ln >> 5, ch = ln & 31;
+        const long long lr = lrow0 + min(q0 + ch, lq - 1);
+        lds_dma4(kh ? dvec + lr : (q0 + ch < lq ? lse + lr : &k3m_inf_word), sl + 2 * BQC * HW);
       }
     }
   };
@@ -587,7 +592,8 @@ __global__ __launch_bounds__(bwd_max_waves<HD>() * 64, 1) void flash_long_bwd2_k
                                       : (long long)ngrp * gridDim.x * lq * HD * 4;
   const __amdgpu_buffer_rsrc_t rdq = __builtin_amdgcn_make_buffer_rsrc(
       ngrp == 1 ? (void*)dq : (void*)dq_ws, (short)0, (int)min(dqbytes, 0x7ffffff0LL), 0x00020000);
-  for (int c = 0; c < NQC; ++c) {
+  // key phase of chunk c (ring slot c % nqb): P and dS of this wave's 32 keys -> dV, dK; dS^T into the image dS
+  auto key_phase = [&](int c, uint16_t* dS) __attribute__((always_inline)) {
     const int q0 = c * BQC;
     const uint16_t* Qc = ring + (c % nqb) * SL;
     const uint16_t* dOc = Qc + BQC * HW;
@@ -638,29 +644,30 @@ __global__ __launch_bounds__(bwd_max_waves<HD>() * 64, 1) void flash_long_bwd2_k
         uint2 wd;
         wd.x = bf_bits(dP[4 * a]) | ((uint32_t)bf_bits(dP[4 * a + 1]) << 16);
         wd.y = bf_bits(dP[4 * a + 2]) | ((uint32_t)bf_bits(dP[4 * a + 3]) << 16);
-        *reinterpret_cast<uint2*>(dSt + ioff<4>(jl, a) + 4 * kl) = wd;
+        *reinterpret_cast<uint2*>(dS + ioff<4>(jl, a) + 4 * kl) = wd;
       }
     } else {
 #pragma unroll
-      for (int a = 0; a < 4; ++a) *reinterpret_cast<uint2*>(dSt + ioff<4>(jl, a) + 4 * kl) = make_uint2(0u, 0u);
+      for (int a = 0; a < 4; ++a) *reinterpret_cast<uint2*>(dS + ioff<4>(jl, a) + 4 * kl) = make_uint2(0u, 0u);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();   // dS^T complete; every read of this chunk's slot done
-    __builtin_amdgcn_sched_barrier(0);
+  };
+  // dQ of chunk cq from its dS^T image dS
+  auto dq_phase = [&](const uint16_t* dS, int cq) __attribute__((always_inline)) {
+    const int q0 = cq * BQC;
     // ---- dQ phase: 16 x 16 tiles dealt to the waves; 4 buffer stores per tile, rows past lq dropped
     for (int t = w; t < NT16; t += nw) {
       const int qt = t & 1, d16 = t >> 1;
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
       int kt = 0;
       for (; kt + 1 < nkt; kt += 2) {
-        const bf16x8 a0 = trfrag16<4>(dSt, 32 * kt, 16 * qt, lane), b0 = trfrag16<NC>(Kimg, 32 * kt, 16 * d16, lane);
-        const bf16x8 a1 = trfrag16<4>(dSt, 32 * kt + 32, 16 * qt, lane);
+        const bf16x8 a0 = trfrag16<4>(dS, 32 * kt, 16 * qt, lane), b0 = trfrag16<NC>(Kimg, 32 * kt, 16 * d16, lane);
+        const bf16x8 a1 = trfrag16<4>(dS, 32 * kt + 32, 16 * qt, lane);
         const bf16x8 b1 = trfrag16<NC>(Kimg, 32 * kt + 32, 16 * d16, lane);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc, 0, 0, 0);
       }
       if (kt < nkt)
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag16<4>(dSt, 32 * kt, 16 * qt, lane),
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag16<4>(dS, 32 * kt, 16 * qt, lane),
                                                       trfrag16<NC>(Kimg, 32 * kt, 16 * d16, lane), acc, 0, 0, 0);
       const int dd = 16 * d16 + (lane & 15);
 #pragma unroll
@@ -676,21 +683,54 @@ __global__ __launch_bounds__(bwd_max_waves<HD>() * 64, 1) void flash_long_bwd2_k
         }
       }
     }
-    // ---- the next chunks: chunk c + nqb into this chunk's slot; chunk c + 1 must have landed before the barrier
-    const bool more = c + nqb < NQC;
-    if (more) dma_chunk(c + nqb);
-    if (c + 1 < NQC) {
-      // vector-memory operations this wave issued after chunk c + 1's DMA: chunks x in [c + 2 - nqb, c] each
-      // stored st_w dQ values and issued n_w DMAs when x + nqb < NQC; a prologue DMA also has the later prologue
-      // chunks after it
-      int younger = 0;
-      const int x0 = c + 2 - nqb;
-      for (int x = x0 < 0 ? 0 : x0; x <= c; ++x) younger += st_w + (x + nqb < NQC ? n_w : 0);
-      if (c + 1 < nqb) younger += n_w * (npre - 1 - (c + 1));
-      vmwait_n(younger);
+  };
+  if constexpr (!DQ2) {
+    for (int c = 0; c < NQC; ++c) {
+      key_phase(c, dSt);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();   // dS^T complete; every read of this chunk's slot done
+      __builtin_amdgcn_sched_barrier(0);
+      dq_phase(dSt, c);
+      // ---- the next chunks: chunk c + nqb into this chunk's slot; chunk c + 1 must have landed before the barrier
+      const bool more = c + nqb < NQC;
+      if (more) dma_chunk(c + nqb);
+      if (c + 1 < NQC) {
+        // vector-memory operations this wave issued after chunk c + 1's DMA: chunks x in [c + 2 - nqb, c] each
+        // stored st_w dQ values and issued n_w DMAs when x + nqb < NQC; a prologue DMA also has the later prologue
+        // chunks after it
+        int younger = 0;
+        const int x0 = c + 2 - nqb;
+        for (int x = x0 < 0 ? 0 : x0; x <= c; ++x) younger += st_w + (x + nqb < NQC ? n_w : 0);
+        if (c + 1 < nqb) younger += n_w * (npre - 1 - (c + 1));
+        vmwait_n(younger);
+      }
+      __builtin_amdgcn_s_barrier();   // chunk c + 1 visible; dS^T free
+      __builtin_amdgcn_sched_barrier(0);
     }
-    __builtin_amdgcn_s_barrier();   // chunk c + 1 visible; dS^T free
-    __builtin_amdgcn_sched_barrier(0);
+  } else {
+    // DQ2: two dS^T images.  Iteration c: (after the barrier that retired chunk c - 1's slot) DMA chunk c - 1 + nqb
+    // into it, the key phase of chunk c into image c & 1, the dQ phase of chunk c - 1 from image (c - 1) & 1, then
+    // one barrier (chunk c + 1 landed, image c & 1 complete, image (c - 1) & 1 free).  A wave whose key phase ends
+    // early goes on to its dQ tiles instead of waiting at a second barrier.
+    for (int c = 0; c < NQC; ++c) {
+      if (c >= 1 && c - 1 + nqb < NQC) dma_chunk(c - 1 + nqb);
+      key_phase(c, dSt + (c & 1) * GK * BQC);
+      if (c >= 1) dq_phase(dSt + ((c - 1) & 1) * GK * BQC, c - 1);
+      if (c + 1 < NQC) {
+        // vector-memory operations this wave issued after chunk c + 1's DMA (issued in iteration i0, or in the
+        // prologue when i0 <= 0): iteration i0's dQ stores, then per iteration x its DMA (if any) and dQ stores
+        int younger = 0;
+        const int i0 = c + 2 - nqb;
+        if (i0 >= 1) younger += st_w;
+        else younger += n_w * (npre - 1 - (c + 1));
+        for (int x = i0 + 1 < 1 ? 1 : i0 + 1; x <= c; ++x) younger += (x - 1 + nqb < NQC ? n_w : 0) + st_w;
+        vmwait_n(younger);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    dq_phase(dSt + ((NQC - 1) & 1) * GK * BQC, NQC - 1);
   }
   if (jv) {
     uint16_t* pv = dv + (krow0 + j) * lddv + hoff + 4 * kl;
@@ -931,10 +971,14 @@ void bwd_groups(int lk, int hd, int& tpg, int& ngrp, int& nw) {
 }
 
 // LDS bytes of flash_long_bwd2_kernel with nqb ring slots
-size_t bwd2_lds(int hd, int nw, int nqb) {
+size_t bwd2_lds(int hd, int nw, int nqb, bool dq2) {
   const size_t HW = hd == 96 ? 128 : hd, GK = 32 * (size_t)nw;
-  return 2 * (2 * GK * HW + GK * BQC) + (size_t)nqb * 2 * (2 * BQC * HW + 128);
+  return 2 * (2 * GK * HW + (dq2 ? 2 : 1) * GK * BQC) + (size_t)nqb * 2 * (2 * BQC * HW + 128);
 }
+
+// K3M_FLASH_LONG_DQ2: 1 (default) two dS^T images in the LDS-DMA backward where they fit (one barrier per query chunk,
+// the dQ tiles of chunk c - 1 beside the key phase of chunk c), 0 one image (two barriers per chunk)
+const int kFlashLongDq2 = k3m_env_int("K3M_FLASH_LONG_DQ2", 1);
 
 // K3M_FLASH_LONG_BWD: 2 (default) the LDS-DMA backward (flash_long_bwd2_kernel), 1 the register-staged one
 const int kFlashLongBwd = k3m_env_int("K3M_FLASH_LONG_BWD", 2);
@@ -953,12 +997,21 @@ void set_attrs() {
     (void)hipFuncSetAttribute((const void*)flash_long_bwd_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_long_bwd_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_long_bwd_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)flash_long_bwd2_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_bwd2_kernel<64, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_bwd2_kernel<64, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_long_fwd2_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_long_fwd2_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_long_fwd2_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)flash_long_bwd2_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)flash_long_bwd2_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_bwd2_kernel<96, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_bwd2_kernel<96, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_bwd2_kernel<128, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_bwd2_kernel<128, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_MAX);
     done = true;
   }
 }
@@ -1052,20 +1105,27 @@ extern "C" int k3m_flash_attn_long_bwd(const void* dctx, long long ldc, const vo
                        (const uint16_t*)dctx, ldc, (const uint16_t*)o, ldo, dvec, nseq, lq, nh, hd);
   const dim3 grid(nseq * nh, ngrp);
   if (kFlashLongBwd == 2) {
-    const int nqb = bwd2_lds(hd, nw, 3) <= (size_t)LDS_MAX ? 3 : 2;
-    const size_t lds2 = bwd2_lds(hd, nw, nqb);
+    const bool dq2 = kFlashLongDq2 != 0 && bwd2_lds(hd, nw, 2, true) <= (size_t)LDS_MAX;
+    const int nqb = bwd2_lds(hd, nw, 3, dq2) <= (size_t)LDS_MAX ? 3 : 2;
+    const size_t lds2 = bwd2_lds(hd, nw, nqb, dq2);
     K3M_ARG(lds2 <= (size_t)LDS_MAX);
     // 32-bit byte offsets of the dQ buffer stores
     K3M_ARG(ngrp > 1 ? (long long)ngrp * rows * hd * 4 < 0x7ffffff0LL
                      : ((long long)nseq * lq) * lddq * 2 < 0x7ffffff0LL);
-#define K3M_FL_BWD2(HD_)                                                                                          \
-    hipLaunchKernelGGL(flash_long_bwd2_kernel<HD_>, grid, dim3(64 * nw), lds2, st, (const uint16_t*)dctx, ldc,      \
+#define K3M_FL_BWD2(HD_, DQ_)                                                                                     \
+    hipLaunchKernelGGL((flash_long_bwd2_kernel<HD_, DQ_>), grid, dim3(64 * nw), lds2, st, (const uint16_t*)dctx, ldc, \
                        (const uint16_t*)q, ldq, (const uint16_t*)k, ldk, (const uint16_t*)v, ldv, kmask, lse, dvec, \
                        (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, lddq, lddk, lddv, dq_ws, lq, lk, nh, tpg, nqb,    \
                        scale, p_drop, seed, off)
-    if (hd == 64) K3M_FL_BWD2(64);
-    else if (hd == 96) K3M_FL_BWD2(96);
-    else K3M_FL_BWD2(128);
+    if (dq2) {
+      if (hd == 64) K3M_FL_BWD2(64, true);
+      else if (hd == 96) K3M_FL_BWD2(96, true);
+      else K3M_FL_BWD2(128, true);
+    } else {
+      if (hd == 64) K3M_FL_BWD2(64, false);
+      else if (hd == 96) K3M_FL_BWD2(96, false);
+      else K3M_FL_BWD2(128, false);
+    }
 #undef K3M_FL_BWD2
   } else {
 #define K3M_FL_BWD(HD_)                                                                                          \
