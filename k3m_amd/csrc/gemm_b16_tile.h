@@ -511,6 +511,17 @@ __device__ __forceinline__ void store8(bf16_t* p, const float (&v)[8]) {
   for (int q = 0; q < 4; ++q) a[q] = (uint32_t)from_f<bf16_t>(v[2 * q]).x | ((uint32_t)from_f<bf16_t>(v[2 * q + 1]).x << 16);
   *reinterpret_cast<u32x4*>(p) = a;
 }
+// non-temporal forms (lab: K3M_B16_LAB bit 2)
+__device__ __forceinline__ void store8_nt(float* p, const float (&v)[8]) {
+  __builtin_nontemporal_store(floatx4{v[0], v[1], v[2], v[3]}, reinterpret_cast<floatx4*>(p));
+  __builtin_nontemporal_store(floatx4{v[4], v[5], v[6], v[7]}, reinterpret_cast<floatx4*>(p + 4));
+}
+__device__ __forceinline__ void store8_nt(bf16_t* p, const float (&v)[8]) {
+  u32x4 a;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) a[q] = (uint32_t)from_f<bf16_t>(v[2 * q]).x | ((uint32_t)from_f<bf16_t>(v[2 * q + 1]).x << 16);
+  __builtin_nontemporal_store(a, reinterpret_cast<u32x4*>(p));
+}
 
 // 8 consecutive C / aux elements as raw registers (prefetched before they are needed)
 template <typename CT> struct Raw8;
@@ -577,7 +588,7 @@ struct NoHookB {
 // persistent walk issues the next tile's first LDS-DMA there; the staging image then must not overlap stage 0).
 template <int TBM, int TBN, int WM, int WN, int EPI, typename CT, typename AccT, class Hook = NoHookB>
 __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint16_t* smem_u16, const AccT& acc,
-                                         int slice, Hook hook = Hook(), bool nostore = false) {
+                                         int slice, Hook hook = Hook(), bool nostore = false, bool ntstore = false) {
   using S = Shape<TBM, TBN, WM, WN>;
   constexpr int WNC = TBN / WN, WS = WNC + AccT::PAD, LPR = WNC / 8, RPP = 64 / LPR, NPS = 32 / RPP, NG = TBM / WM / 32;
   constexpr int RING = sizeof(CT) == 2 ? 2 : 1;   // passes the per-pass loads run ahead (register budget)
@@ -653,6 +664,9 @@ __device__ __forceinline__ void epilogue(const K3mGemm& g, int m0, int n0, uint1
           if (nostore) {   // lab timing (K3M_B16_LAB bit 0): the math stays live, nothing is written
 #pragma unroll
             for (int e = 0; e < 8; ++e) asm volatile("" ::"v"(o[e]), "v"(pa[e]));
+          } else if (ntstore) {
+            store8_nt(C + row * ldc + col, o);
+            if constexpr (EPI == K3M_EPI_BIAS_GELU) store8_nt(aux + row * g.ldaux + col, pa);
           } else {
             store8(C + row * ldc + col, o);
             if constexpr (EPI == K3M_EPI_BIAS_GELU) store8(aux + row * g.ldaux + col, pa);
@@ -848,7 +862,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_persist_kernel(GemmGroup
     const uint64_t until = t0 + (uint64_t)(blockIdx.x & 3) * (uint64_t)grp.stagger;
     while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(8);
   }
-  const bool nostore = (grp.lab & 1) != 0;
+  const bool nostore = (grp.lab & 1) != 0, ntstore = (grp.lab & 4) != 0;
   PUnit<TBM, TBN, WM, WN> cur;
   cur.decode(grp, u);
   bool pre = false;
@@ -883,10 +897,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_persist_kernel(GemmGroup
           lb.issue(smem + TBM * BK);
         }
       };
-      epilogue<TBM, TBN, WM, WN, EPI, CT>(g, cur.m0, cur.n0, smem + EOFF, acc, cur.slice, hook, nostore);
+      epilogue<TBM, TBN, WM, WN, EPI, CT>(g, cur.m0, cur.n0, smem + EOFF, acc, cur.slice, hook, nostore, ntstore);
       next_pre = issue;
     } else {
-      epilogue<TBM, TBN, WM, WN, EPI, CT>(g, cur.m0, cur.n0, smem, acc, cur.slice, NoHookB(), nostore);
+      epilogue<TBM, TBN, WM, WN, EPI, CT>(g, cur.m0, cur.n0, smem, acc, cur.slice, NoHookB(), nostore, ntstore);
     }
     if (!more) break;
     u = nu;

@@ -477,7 +477,8 @@ int b16_cus() {
 const bool kB16Prefetch = k3m_env_flag("K3M_B16_PREFETCH", false);
 
 // timing-only lab knobs of the persistent walk (never set in product runs): K3M_B16_LAB bit 0 = skip the C / aux
-// stores, bit 1 = staggered start of K3M_B16_STAGGER ticks (10 ns) per workgroup group (b & 3)
+// stores, bit 1 = staggered start of K3M_B16_STAGGER ticks (10 ns) per workgroup group (b & 3), bit 2 = non-temporal
+// C / aux stores in the interior-tile epilogue
 const int kB16Lab = k3m_env_int("K3M_B16_LAB", 0);
 const int kB16Stagger = k3m_env_int("K3M_B16_STAGGER", 500);
 
