@@ -759,7 +759,9 @@ __global__ __launch_bounds__(bwd_max_waves<HD>() * 64, 1) void flash_long_bwd2_k
 template <int HD> constexpr int fwd2_nkb() { return HD == 64 ? 3 : 2; }
 template <int HD> constexpr int fwd2_occ() { return HD == 64 ? 3 : 2; }
 
-template <int HD>
+// DROP: the p > 0 form (a template parameter: with both loops in one kernel the d = 64 form spilled 27 registers
+// at its 168-register budget, and the reloads' vmcnt(0) drained the DMA ring every chunk)
+template <int HD, bool DROP>
 __global__ __launch_bounds__(FNT, fwd2_occ<HD>()) void flash_long_fwd2_kernel(
     const uint16_t* __restrict__ q, long long ldq, const uint16_t* __restrict__ k, long long ldk,
     const uint16_t* __restrict__ v, long long ldv, const float* __restrict__ kmask, uint16_t* __restrict__ ctx,
@@ -791,11 +793,13 @@ __global__ __launch_bounds__(FNT, fwd2_occ<HD>()) void flash_long_fwd2_kernel(
   const long long prow = ((long long)s * nh + h) * lq + min(i, lq - 1);
   auto dma_chunk = [&](int c) {   // K and V rows c FKC .. + FKC - 1 (clamped) into slot c % NKB
     uint16_t* Kb = ring + (c % NKB) * 2 * FKC * HW;
+    int ln = lane;   // opaque: the per-lane offsets are recomputed here instead of hoisted (and spilled) by the loop
+    asm volatile("" : "+v"(ln));
 #pragma unroll
     for (int t = 0; t < N_W; ++t) {
       const int inst = w + NWF * t;   // 0 .. 2 CI - 1: K first, then V
-      if (inst < CI) dma_rows<NC, NCL>(Kb, inst * RPI, k, ldk, krow0 + c * FKC, lk - c * FKC, hoff, lane);
-      else dma_rows<NC, NCL>(Kb + FKC * HW, (inst - CI) * RPI, v, ldv, krow0 + c * FKC, lk - c * FKC, hoff, lane);
+      if (inst < CI) dma_rows<NC, NCL>(Kb, inst * RPI, k, ldk, krow0 + c * FKC, lk - c * FKC, hoff, ln);
+      else dma_rows<NC, NCL>(Kb + FKC * HW, (inst - CI) * RPI, v, ldv, krow0 + c * FKC, lk - c * FKC, hoff, ln);
     }
   };
   const int npre = min(NKB - 1, nkc);
@@ -854,9 +858,12 @@ __global__ __launch_bounds__(FNT, fwd2_occ<HD>()) void flash_long_fwd2_kernel(
       // c FKC + 32 jt + 8 q + 4 kl + b: pairs (b = 0, 1) and (2, 3) of one draw each, pair counters
       // pb + 16 jt + 4 q + b / 2 from this lane's first pair pb; the high word is mixed once per chunk, for pb's high
       // word and for the next one (a pair whose low word carried)
-      if (dr.thr != 0u) {
+      if constexpr (DROP) {
         const uint64_t pb = off + (uint64_t)prow * (uint64_t)((lk + 1) >> 1) + (uint64_t)(c * (FKC / 2) + 2 * kl);
-        const uint32_t lo = (uint32_t)pb, pre0 = k3m_pair_pre(dr.key, pb), pre1 = k3m_pair_pre(dr.key, pb + (1ull << 32));
+        uint32_t lo = (uint32_t)pb, pre0 = k3m_pair_pre(dr.key, pb), pre1 = k3m_pair_pre(dr.key, pb + (1ull << 32));
+        // opaque: otherwise the compiler sinks the high-word multiply below the carry select, one more 32-bit
+        // multiply per pair
+        asm volatile("" : "+v"(lo), "+v"(pre0), "+v"(pre1));
 #pragma unroll
         for (int jt = 0; jt < FKC / 32; ++jt)
 #pragma unroll
@@ -1001,9 +1008,18 @@ void set_attrs() {
                               LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_long_bwd2_kernel<64, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)flash_long_fwd2_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)flash_long_fwd2_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)flash_long_fwd2_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_fwd2_kernel<64, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_fwd2_kernel<64, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_fwd2_kernel<96, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_fwd2_kernel<96, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_fwd2_kernel<128, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)flash_long_fwd2_kernel<128, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_long_bwd2_kernel<96, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_MAX);
     (void)hipFuncSetAttribute((const void*)flash_long_bwd2_kernel<96, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1034,13 +1050,14 @@ extern "C" int k3m_flash_attn_long_fwd(const void* q, long long ldq, const void*
   const dim3 grid(nseq * nh, (lq + FNT / 2 - 1) / (FNT / 2));
   if (kFlashLongFwd == 2 && fwd2_lds(lk, hd) <= (size_t)LDS_MAX) {
     const size_t lds2 = fwd2_lds(lk, hd);
-#define K3M_FL_FWD2(HD_)                                                                                          \
-    hipLaunchKernelGGL(flash_long_fwd2_kernel<HD_>, grid, dim3(FNT), lds2, st, (const uint16_t*)q, ldq,          \
+    const bool drop = p_drop > 0.f;   // k3m_drop_init: thr != 0 iff p > 0
+#define K3M_FL_FWD2(HD_, DR_)                                                                                     \
+    hipLaunchKernelGGL((flash_long_fwd2_kernel<HD_, DR_>), grid, dim3(FNT), lds2, st, (const uint16_t*)q, ldq,   \
                        (const uint16_t*)k, ldk, (const uint16_t*)v, ldv, kmask, (uint16_t*)ctx, ldc, lse, lq, lk, nh, \
                        scale, p_drop, seed, off)
-    if (hd == 64) K3M_FL_FWD2(64);
-    else if (hd == 96) K3M_FL_FWD2(96);
-    else K3M_FL_FWD2(128);
+    if (hd == 64) { if (drop) K3M_FL_FWD2(64, true); else K3M_FL_FWD2(64, false); }
+    else if (hd == 96) { if (drop) K3M_FL_FWD2(96, true); else K3M_FL_FWD2(96, false); }
+    else { if (drop) K3M_FL_FWD2(128, true); else K3M_FL_FWD2(128, false); }
 #undef K3M_FL_FWD2
     K3M_CHECK_LAUNCH();
     return 0;
