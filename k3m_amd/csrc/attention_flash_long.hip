@@ -766,7 +766,7 @@ __global__ __launch_bounds__(FNT, fwd2_occ<HD>()) void flash_long_fwd2_kernel(
     const uint16_t* __restrict__ q, long long ldq, const uint16_t* __restrict__ k, long long ldk,
     const uint16_t* __restrict__ v, long long ldv, const float* __restrict__ kmask, uint16_t* __restrict__ ctx,
     long long ldc, float* __restrict__ lse, int lq, int lk, int nh, float scale, float p_drop, uint64_t seed,
-    uint64_t off) {
+    uint64_t off, int xcdmap) {
   using G = Geo<HD>;
   constexpr int NCL = G::NCL, NC = G::NC, HW = G::HW, DT = G::DT, KS = G::KS;
   constexpr int NKB = fwd2_nkb<HD>();
@@ -778,13 +778,22 @@ __global__ __launch_bounds__(FNT, fwd2_occ<HD>()) void flash_long_fwd2_kernel(
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* ring = smem;                                            // NKB x {K [FKC][HW], V [FKC][HW]}
   float* msk = reinterpret_cast<float*>(ring + NKB * 2 * FKC * HW);   // [LKP] mask * log2 e, -inf past lk
-  const int s = blockIdx.x / nh, h = blockIdx.x % nh;
+  // workgroup -> (sequence x head, query block).  xcdmap (the head count a multiple of 8): the query blocks of one
+  // head get consecutive ids on ONE XCD (ids n, n + 8, ...; workgroups are dealt to the 8 XCDs round-robin), so they
+  // run together and read that head's K / V rows through the same L2 instead of once each from HBM
+  int hx = blockIdx.x, qb = blockIdx.y;
+  if (xcdmap) {
+    const int n = blockIdx.x + gridDim.x * blockIdx.y, loc = n >> 3;
+    hx = (loc / (int)gridDim.y) * 8 + (n & 7);
+    qb = loc % (int)gridDim.y;
+  }
+  const int s = hx / nh, h = hx % nh;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, cl = lane & 31, kl = lane >> 5;
   const int nkc = (lk + FKC - 1) / FKC, LKP = nkc * FKC;
   const long long qrow0 = (long long)s * lq, krow0 = (long long)s * lk;
   const int hoff = h * HD;
-  const int qw0 = blockIdx.y * (FNT / 2) + 32 * w;
+  const int qw0 = qb * (FNT / 2) + 32 * w;
   const bool wact = qw0 < lq;
   const int i = qw0 + cl;
   const bool iv = i < lq;
@@ -963,6 +972,8 @@ size_t fwd2_lds(int lk, int hd) {
 }
 // K3M_FLASH_LONG_FWD: 2 (default) the LDS-DMA forward (flash_long_fwd2_kernel), 1 the register-staged one
 const int kFlashLongFwd = k3m_env_int("K3M_FLASH_LONG_FWD", 2);
+// K3M_FLASH_LONG_XCD: 1 (default) the LDS-DMA forward deals the query blocks of a head to one XCD (flash_long_fwd2_kernel)
+const int kFlashLongXcd = k3m_env_int("K3M_FLASH_LONG_XCD", 1);
 
 // key tiles per group and groups of a head's backward
 // K3M_FLASH_LONG_TPG (lab A/B): at most this many 32-key tiles per backward workgroup (0: as many as fit)
@@ -1051,10 +1062,11 @@ extern "C" int k3m_flash_attn_long_fwd(const void* q, long long ldq, const void*
   if (kFlashLongFwd == 2 && fwd2_lds(lk, hd) <= (size_t)LDS_MAX) {
     const size_t lds2 = fwd2_lds(lk, hd);
     const bool drop = p_drop > 0.f;   // k3m_drop_init: thr != 0 iff p > 0
+    const int xcdmap = kFlashLongXcd && (nseq * nh) % 8 == 0 ? 1 : 0;
 #define K3M_FL_FWD2(HD_, DR_)                                                                                     \
     hipLaunchKernelGGL((flash_long_fwd2_kernel<HD_, DR_>), grid, dim3(FNT), lds2, st, (const uint16_t*)q, ldq,   \
                        (const uint16_t*)k, ldk, (const uint16_t*)v, ldv, kmask, (uint16_t*)ctx, ldc, lse, lq, lk, nh, \
-                       scale, p_drop, seed, off)
+                       scale, p_drop, seed, off, xcdmap)
     if (hd == 64) { if (drop) K3M_FL_FWD2(64, true); else K3M_FL_FWD2(64, false); }
     else if (hd == 96) { if (drop) K3M_FL_FWD2(96, true); else K3M_FL_FWD2(96, false); }
     else { if (drop) K3M_FL_FWD2(128, true); else K3M_FL_FWD2(128, false); }
