@@ -200,19 +200,18 @@ def test_nan_loss_fails_fast(dev):
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_overlapped_optimizer_bit_identical(dev, dtype):
+def test_overlapped_optimizer_bit_identical(dev, dtype, deterministic):
     """The per-block AdamW on the side stream (Trainer.overlap, K3M_OPT_OVERLAP) updates every element exactly as
-    the one sweep after the backward (AdamW is elementwise; the blocks only re-cut the runs).
-
-    The backward itself is not bit-reproducible run to run (the structure aggregator's and the embedding
-    backward's float atomics, like the reference's index_add_ on the GPU), so the check is split in two:
+    the one sweep after the backward (AdamW is elementwise; the blocks only re-cut the runs).  Two checks:
     * mechanics, bit-exact: the gradients each block's AdamW consumed are captured at hand-off; a twin trainer
       restored to the same pre-step state runs the one sweep on exactly those gradients, and parameters, both
       moments and the bf16 shadow agree bit for bit after each of three steps; every optimised element is
       covered by exactly one block run; the gradient buffer is zero afterwards;
-    * hand-off timing: the captured gradients match a sweep run's final gradients to the run-to-run rounding
-      of the atomics (1e-3 of each tensor's max + 1e-8: the attention key biases' gradient is zero up to rounding), i.e. no block was read before the backward finished it (fp32 only: with a bf16 encoder the atomics'
-      rounding flips bf16 roundings downstream, 0.5% of a tensor's max run to run; the hand-offs are the same)."""
+    * hand-off timing, bit-exact: under K3M_DETERMINISTIC (the fixed-order embedding / structure-aggregator / LPM
+      backward) the captured gradients equal a sweep run's final gradients, i.e. no block was read before the
+      backward finished it.  (With the float-atomic backward this compared to a tolerance, 1e-3 of each tensor's
+      max + 1e-8, which the structure head's output bias -- a gradient that is zero up to rounding, its scores
+      entering a softmax -- exceeded once by run-to-run rounding alone: 1.24e-8.)"""
     from k3m_amd.trainer import Trainer
     from k3m_amd.synthetic import synthetic_batch, synthetic_noise
     cfg = _no_dropout_cfg()
@@ -265,13 +264,12 @@ def test_overlapped_optimizer_bit_identical(dev, dtype):
             for a, n, _, _ in ta.runs:
                 assert torch.equal(fa.data16[a:a + n], fb.data16[a:a + n]), (k, a, n)
         bad = []
-        for name, shape in (fa.spec if dtype == "fp32" else ()):
+        for name, shape in fa.spec:
             o = fa.offsets[name]
             n = math.prod(shape)
             x, y = cap[o:o + n], final_c[k][o:o + n]
-            tol = 1e-3 * float(y.abs().max()) + 1e-8   # key biases: gradient zero up to rounding
-            if float((x - y).abs().max()) > tol:
-                bad.append((name, float((x - y).abs().max()), tol))
+            if not torch.equal(x, y):
+                bad.append((name, float((x - y).abs().max()), float(y.abs().max())))
         assert not bad, (k, bad[:10])
     cover = torch.zeros(fa.data.numel(), dtype=torch.int32)
     for runs in ta.block_runs.values():
