@@ -28,6 +28,7 @@ using namespace k3m_flash;
 
 constexpr int NW = 4, NT = NW * 64;
 constexpr int MAXL = 128;
+constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
 
 // stage rows [row0, row0 + nrows) x [coff, coff + 8 NC) of a bf16 matrix into an image
 // (rows >= nvalid zero); all loads issued before the LDS writes
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __rest
     }
     const int t = threadIdx.x;
     float mv = 0.f;
-    if (t < LKh) mv = t < lk ? (kmask ? kmask[krow0 + t] : 0.f) : -INFINITY;
+    if (t < LKh) mv = t < lk ? (kmask ? kmask[krow0 + t] * kLog2e : 0.f) : -INFINITY;   // exp2 domain
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int e = threadIdx.x + u * NT, i = e / NCL, c = e % NCL;
@@ -135,8 +136,10 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __rest
       S[jt] = a;
     }
   }
-  // softmax over j (registers x lane halves) for query i = i0 + cl
+  // softmax over j (registers x lane halves) for query i = i0 + cl, in the exp2 domain (scores and mask pre-scaled
+  // by log2 e: one multiply per score less than exp(x - max))
   const int i = i0 + cl;
+  const float sl2 = scale * kLog2e;
   float mx = -INFINITY;
 #pragma unroll
   for (int jt = 0; jt < MAXL / 32; ++jt)
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __rest
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int j = 32 * jt + (r & 3) + 8 * (r >> 2) + 4 * kl;
-        const float x = S[jt][r] * scale + msk[j];
+        const float x = fmaf(S[jt][r], sl2, msk[j]);
         S[jt][r] = x;
         mx = fmaxf(mx, x);
       }
@@ -156,7 +159,7 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __rest
     if (jt < NJT) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float e = __expf(S[jt][r] - mx);
+        const float e = __builtin_amdgcn_exp2f(S[jt][r] - mx);
         S[jt][r] = e;
         sum += e;
       }
@@ -164,13 +167,16 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __rest
   sum += __shfl_xor(sum, 32, 64);
   const float inv = 1.f / sum;
   const long long prow = ((long long)s * nh + h) * lq + i;   // row of the [nseq, nh, lq] LSE
-  if (kl == 0 && i < lq) lse[prow] = mx + __logf(sum);
+  if (kl == 0 && i < lq) lse[prow] = mx * kLn2 + __logf(sum);
   if (p_drop > 0.f) {
     // registers 4 q + b of tile jt are keys 32 jt + 8 q + 4 kl + b: pairs (b = 0, 1), (2, 3) share one draw, pair
     // counter pb + 16 jt + 4 q + b / 2 (k3m_attn_drop), the high word mixed once (and once more for a carry)
     const K3mDrop dr = k3m_drop_init(seed, p_drop);
     const uint64_t pb = off + (uint64_t)prow * (uint64_t)((lk + 1) >> 1) + (uint64_t)(2 * kl);
-    const uint32_t lo = (uint32_t)pb, pre0 = k3m_pair_pre(dr.key, pb), pre1 = k3m_pair_pre(dr.key, pb + (1ull << 32));
+    uint32_t lo = (uint32_t)pb, pre0 = k3m_pair_pre(dr.key, pb), pre1 = k3m_pair_pre(dr.key, pb + (1ull << 32));
+    asm volatile("" : "+v"(lo), "+v"(pre0), "+v"(pre1));   // (the high-word multiply stays out of the pair loop)
+    // padding keys carry P = 0 (their mask is -inf) and padding query rows are never stored: no per-score bounds test
+    const float invs = inv * dr.scale;
 #pragma unroll
     for (int jt = 0; jt < MAXL / 32; ++jt)
       if (jt < NJT) {
@@ -182,9 +188,8 @@ __global__ __launch_bounds__(NT, 2) void flash_fwd_kernel(const uint16_t* __rest
             const uint32_t hh = k3m_mix32(x ^ (x < lo ? pre1 : pre0));
 #pragma unroll
             for (int b2 = 0; b2 < 2; ++b2) {
-              const int r = 4 * q + 2 * hb + b2, j = 32 * jt + 8 * q + 4 * kl + 2 * hb + b2;
-              const bool kept = i < lq && j < lk && k3m_attn_half(hh, b2) >= dr.thr16;
-              S[jt][r] = kept ? S[jt][r] * inv * dr.scale : 0.f;
+              const int r = 4 * q + 2 * hb + b2;
+              S[jt][r] = k3m_attn_half(hh, b2) >= dr.thr16 ? S[jt][r] * invs : 0.f;
             }
           }
       }
